@@ -1,0 +1,226 @@
+"""Benchmark: Mrays/s of the wavefront integrator on the C3 room scene
+(BASELINE.json metric "Mrays/s + Msamples/s, Viking Room 1920x1080 1024spp").
+
+A step is one integrator round (extend + shade over every pixel slot, i.e.
+one RunBasicRenderer(1)).  Inputs (scene, slot state) are resident in HBM
+before timing starts.  For N GPUs (one process per GPU, launched by
+torch.distributed.run) each rank owns 16-row bands of a 1920 x (1080*N)
+frame, so per-GPU work is fixed (weak scaling); the frame-end RCCL reduce of
+the float4 accumulator to rank 0 is inside the timed region.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib.util
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+PKG_DIR = ROOT / "path-tracer_amd"
+
+HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# Algorithmic bytes per slot per launch (DESIGN.md "Roofline"): extend reads
+# the 16-B ray record and writes the 16-B hit record + 8-B UV; shade reads
+# ray 16 + hit 16 + uv 8 + path 56 and writes ray 16 + path 56.
+ALG_BYTES = {"extend": 40, "shade": 168}
+PATH_BYTES_PER_RAY = 220  # SURVEY.md §8(d) whole-path definition
+
+
+def load_package():
+    spec = importlib.util.spec_from_file_location("path_tracer_amd", PKG_DIR / "__init__.py",
+                                                  submodule_search_locations=[str(PKG_DIR)])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["path_tracer_amd"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def cpu_baseline(pt, scene, width, height, max_seconds=12.0, max_rounds=6):
+    """Time the CPU oracle (scalar C++ restatement, std::thread over host
+    cores) on the same scene and frame.  Bounded: Reset + Run(2) warm-up, then
+    single rounds until max_seconds of timed work or max_rounds."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    o = oracle_lib.OracleRenderer(scene.packs(), width, height, threads=threads)
+    o.RenderFlags = 3
+    o.reset()
+    o.run(2)
+    r0, s0 = o.counters()
+    t0 = time.perf_counter()
+    rounds = 0
+    while rounds < max_rounds:
+        o.run(1)
+        rounds += 1
+        if time.perf_counter() - t0 > max_seconds:
+            break
+    dt = time.perf_counter() - t0
+    r1, s1 = o.counters()
+    o.close()
+    return {
+        "value": round((r1 - r0) / dt / 1e6, 4),
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"C3 {width}x{height}, {rounds} rounds after Reset+Run(2) warm-up "
+                  f"({(r1 - r0)} rays, {(s1 - s0)} samples, {dt:.1f} s)",
+        "msamples_per_s": round((s1 - s0) / dt / 1e6, 4),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=128)
+    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    pt = load_package()
+    scene = pt.Scene.config(args.config)
+    info = scene.info
+    width, height = info.width, info.height * world
+
+    dev = pt.Device(local_rank)
+    dscene = pt.DeviceScene(dev)
+    dscene.update(scene)
+    sb = pt.SampleBuffer(dev, width, height)
+    r = pt.BasicRenderer(dev, dscene, sb, rank=rank, nranks=world)
+    r.RenderFlags = info.render_flags
+    r.PathTerminationProbability = info.termination_probability
+    comm = None
+    if world > 1:
+        import torch
+        uid = bytearray(pt.Comm.unique_id()) if rank == 0 else bytearray(128)
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        dist.broadcast(t, 0)
+        comm = pt.Comm(dev, world, rank, bytes(t.tolist()))
+
+    # Reset + Run(2) as after a restart (application.cpp:109-110), then warm-up.
+    r.reset()
+    r.run(2)
+    for _ in range(args.warmup):
+        r.run(1)
+    dev.synchronize()
+    alpha0 = float(sb.read()[..., 3].sum(dtype=np.float64))
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    dev.set_profiling(True)
+    dev.reset_kernel_stats()
+    barrier()
+    dev.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r.run(1)
+    if comm is not None:
+        comm.reduce_sample_buffer(sb, 0)
+    dev.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    n_ext, ms_ext = dev.kernel_stats(1)
+    n_sh, ms_sh = dev.kernel_stats(2)
+    dev.set_profiling(False)
+
+    slots_owned = int(np.sum(pt.owned_pixels(width, height, rank, world)))
+    acc = sb.read()
+    if comm is None:
+        samples = float(acc[..., 3].sum(dtype=np.float64)) - alpha0
+    else:
+        samples = None   # computed below from the per-rank counts
+
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        local = torch.tensor([float(slots_owned), alpha0], dtype=torch.float64)
+        dist.all_reduce(local, op=dist.ReduceOp.SUM)
+        total_slots, alpha0_total = float(local[0]), float(local[1])
+        if rank == 0:
+            samples = float(acc[..., 3].sum(dtype=np.float64)) - alpha0_total
+    else:
+        total_slots = float(slots_owned)
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    rays = total_slots * args.steps
+    mrays = rays / dt / 1e6
+    avg_ext = ms_ext / max(n_ext, 1)
+    avg_sh = ms_sh / max(n_sh, 1)
+    kernels = {
+        "extend": {"avg_ms": avg_ext, "gbps": ALG_BYTES["extend"] * slots_owned / (avg_ext * 1e-3) / 1e9},
+        "shade": {"avg_ms": avg_sh, "gbps": ALG_BYTES["shade"] * slots_owned / (avg_sh * 1e-3) / 1e9},
+    }
+    dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
+    achieved = kernels[dom]["gbps"]
+    out = {
+        "metric": "Mrays/s (Viking Room 1920x1080, 1024spp)",
+        "value": round(mrays, 3),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (procedural 3,948-triangle room mesh + 1024^2 texture; Viking Room asset absent)",
+        "config": {
+            "workload": f"C{args.config} room scene, {width}x{height} px ({info.width}x{info.height} per GPU), "
+                        f"one round (extend+shade) per step, 16-row bands over {world} GPU(s)",
+            "spp_target": info.spp,
+            "mesh_faces": info.mesh_face_count,
+            "parallelism": f"pixel-bands x{world}" + (" + RCCL reduce" if world > 1 else ""),
+        },
+        "msamples_per_s": round(samples / dt / 1e6, 3) if samples is not None else None,
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dom,
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 5),
+            "traffic": None,
+            "alg_bytes_per_slot": ALG_BYTES[dom],
+            "launch_avg_ms": {"extend": round(avg_ext, 4), "shade": round(avg_sh, 4)},
+            "path_gbps_220B_per_ray": round(PATH_BYTES_PER_RAY * rays / dt / 1e9, 2),
+        },
+    }
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(pt, scene, info.width, info.height)
+    print(json.dumps(out), flush=True)
+    for x in (r, sb, dscene):
+        x.close()
+    if comm is not None:
+        comm.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,144 @@
+/*
+ * pt_api.h — C ABI of the MI355X wavefront path tracer (libpathtracer.so).
+ *
+ * Drop-in for the reference's integrator boundary.  Each entry point names the
+ * reference interface it replaces (paths relative to the reference root):
+ *
+ *   ptCreateDevice            src/core/vulkan.hpp  CreateVulkan (device + queue)
+ *   ptCreateScene             src/scene/scene.hpp:440  CreateVulkanScene
+ *   ptUpdateScene             src/scene/scene.hpp:441  UpdateVulkanScene
+ *   ptDestroyScene            src/scene/scene.hpp:442  DestroyVulkanScene
+ *   ptCreateSampleBuffer      src/integrator/integrator.hpp:51  CreateSampleBuffer
+ *   ptDestroySampleBuffer     src/integrator/integrator.hpp:53  DestroySampleBuffer
+ *   ptCreateBasicRenderer     src/integrator/basic.hpp:28  CreateBasicRenderer
+ *   ptDestroyBasicRenderer    src/integrator/basic.hpp:29  DestroyBasicRenderer
+ *   ptResetBasicRenderer      src/integrator/basic.hpp:31  ResetBasicRenderer
+ *   ptRunBasicRenderer        src/integrator/basic.hpp:32  RunBasicRenderer
+ *   ptBasicRendererParams     src/integrator/basic.hpp:6-26  (the caller-written
+ *                             CameraIndex / RenderFlags / PathLengthLimit /
+ *                             PathTerminationProbability fields, FrameIndex)
+ *
+ * Additions (no reference counterpart): sample-buffer readback, explicit
+ * synchronisation, a bit-exact ray query (ptTraceRays), slot-state readback,
+ * per-kernel timing, pixel-band partitioning and an RCCL frame-end reduce for
+ * one-process-per-GPU rendering.
+ *
+ * Conventions: creators return NULL on failure and set ptGetLastError();
+ * other calls return 0 on success or a non-zero status (HIP / RCCL error
+ * codes are forwarded).  ptDestroy* accept NULL.  Reset/Run enqueue work on
+ * the device's stream and return immediately (the reference records into a
+ * command buffer that executes after submit); reads and ptSynchronize block.
+ */
+#ifndef PT_API_H
+#define PT_API_H
+
+#include <stdint.h>
+#include "pt_packed.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pt_device pt_device;
+typedef struct pt_scene pt_scene;
+typedef struct pt_sample_buffer pt_sample_buffer;
+typedef struct pt_basic_renderer pt_basic_renderer;
+typedef struct pt_comm pt_comm;
+
+/* Mutable renderer state (src/integrator/basic.hpp:18-25).  The caller writes
+ * CameraIndex, RenderFlags, PathLengthLimit and PathTerminationProbability
+ * before Reset/Run, exactly like application.cpp:104-107.  FrameIndex is the
+ * seed schedule: Reset seeds with the current value, Run increments it first
+ * and all rounds of one Run share the seed (basic.cpp:285-332). */
+typedef struct pt_basic_renderer_params {
+    uint32_t FrameIndex;
+    uint32_t CameraIndex;
+    uint32_t RenderFlags;                 /* PT_RENDER_FLAG_ACCUMULATE | _SAMPLE_JITTER */
+    uint32_t PathLengthLimit;             /* unused by the reference integrator */
+    float    PathTerminationProbability;
+} pt_basic_renderer_params;
+
+/* One trace result (src/integrator/basic.glsl.inc:32-38).  On a miss only
+ * shape_material (= 0xFFFFFFFF) is meaningful, as in StoreTraceHit. */
+typedef struct pt_hit_record {
+    float    time;
+    uint32_t shape_material;              /* shape << 16 | material */
+    uint32_t packed_normal;               /* octahedral snorm16x2 */
+    uint32_t packed_tangent;
+    float    u, v;
+} pt_hit_record;
+
+/* Per-pixel integrator state (trace_buffer + path_buffer of
+ * src/integrator/basic.glsl.inc:23-59), in image order.  Duration is not
+ * stored: every producer writes HIT_TIME_LIMIT (scene.glsl.inc:617,
+ * basic_scatter.glsl:163,307). */
+typedef struct pt_pixel_state {
+    float    origin[3];
+    uint32_t packed_velocity;
+    pt_hit_record hit;
+    float    lambda0;
+    float    throughput[4];
+    float    probability[4];
+    float    sample[3];
+    uint32_t active01, active23;          /* 4 x u16 active shape stack, 0xFFFF = none */
+} pt_pixel_state;
+
+enum {
+    PT_KERNEL_RAYGEN = 0,
+    PT_KERNEL_EXTEND = 1,
+    PT_KERNEL_SHADE  = 2,
+    PT_KERNEL_COUNT  = 3,
+};
+
+const char* ptGetLastError(void);
+
+pt_device* ptCreateDevice(int hip_device);
+void       ptDestroyDevice(pt_device* device);
+int        ptSynchronize(pt_device* device);
+int        ptGetDeviceCount(int* count);
+
+pt_scene* ptCreateScene(pt_device* device);
+int       ptUpdateScene(pt_device* device, pt_scene* scene, const pt_scene_packs* packs, uint32_t dirty_flags);
+void      ptDestroyScene(pt_device* device, pt_scene* scene);
+
+pt_sample_buffer* ptCreateSampleBuffer(pt_device* device, uint32_t width, uint32_t height);
+void              ptDestroySampleBuffer(pt_device* device, pt_sample_buffer* buffer);
+/* rgba = width*height*4 floats: CIE XYZ sums + sample count, row-major. */
+int               ptReadSampleBuffer(pt_device* device, pt_sample_buffer* buffer, float* rgba);
+
+pt_basic_renderer* ptCreateBasicRenderer(pt_device* device, pt_scene* scene, pt_sample_buffer* buffer);
+/* Renderer owning only the 16-row pixel bands b with b % nranks == rank. */
+pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* device, pt_scene* scene, pt_sample_buffer* buffer,
+                                                    uint32_t rank, uint32_t nranks);
+void               ptDestroyBasicRenderer(pt_device* device, pt_basic_renderer* renderer);
+pt_basic_renderer_params* ptBasicRendererParams(pt_basic_renderer* renderer);
+int                ptResetBasicRenderer(pt_device* device, pt_basic_renderer* renderer);
+int                ptRunBasicRenderer(pt_device* device, pt_basic_renderer* renderer, uint32_t rounds);
+uint32_t           ptBasicRendererSlotCount(pt_basic_renderer* renderer);
+/* out = width*height states in image order; pixels outside the renderer's
+ * partition are left untouched. */
+int                ptReadBasicRendererState(pt_device* device, pt_basic_renderer* renderer, pt_pixel_state* out);
+
+/* Bit-exact Trace() (scene.glsl.inc:522-611) of n rays: origins (3n floats),
+ * packed unit velocities (n), durations (n) -> n hit records. */
+int ptTraceRays(pt_device* device, pt_scene* scene, uint32_t n, const float* origins,
+                const uint32_t* packed_velocities, const float* durations, pt_hit_record* out);
+
+/* Per-kernel device time, measured with HIP events on the renderer stream. */
+int ptSetProfiling(pt_device* device, int enable);
+int ptGetKernelStats(pt_device* device, int kernel, uint64_t* launches, double* total_ms);
+int ptResetKernelStats(pt_device* device);
+
+/* RCCL communicator over one process per GPU (xGMI). */
+int      ptCommGetUniqueId(uint8_t id[128]);
+pt_comm* ptCommCreate(pt_device* device, int nranks, int rank, const uint8_t id[128]);
+void     ptCommDestroy(pt_comm* comm);
+/* Frame-end ncclReduce(sum) of the float4 accumulator to `root` (exact: the
+ * ranks' pixel bands are disjoint). */
+int      ptCommReduceSampleBuffer(pt_device* device, pt_comm* comm, pt_sample_buffer* buffer, int root);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PT_API_H */

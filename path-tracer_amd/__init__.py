@@ -1,0 +1,18 @@
+"""MI355X-native wavefront path tracer (drop-in for the integrator of
+samukallio/path-tracer): host scene API + HIP/gfx950 kernels behind a C ABI.
+
+Import as `path_tracer_amd` via the loader in tests/conftest.py or bench.py
+(the directory name contains a hyphen).
+"""
+from . import _native
+from .scene import (Scene, spectrum_coefficients, build_spectrum_table, load_spectrum_table, mesh_depth,
+                    mesh_node_count, ENTITY_CONTAINER, ENTITY_CAMERA, ENTITY_MESH_INSTANCE, ENTITY_PLANE,
+                    ENTITY_SPHERE, ENTITY_CUBE, MATERIAL_BASIC_DIFFUSE, MATERIAL_BASIC_METAL,
+                    MATERIAL_BASIC_TRANSLUCENT, MATERIAL_OPENPBR, TEXTURE_RAW, TEXTURE_REFLECTANCE_WITH_ALPHA,
+                    TEXTURE_RADIANCE, SCENE_DIRTY_ALL, RENDER_FLAG_ACCUMULATE, RENDER_FLAG_SAMPLE_JITTER)
+from .integrator import (Device, DeviceScene, SampleBuffer, BasicRenderer, Comm, PathTracerError, device_count,
+                         CreateSampleBuffer, CreateBasicRenderer, ResetBasicRenderer, RunBasicRenderer,
+                         DestroyBasicRenderer, DestroySampleBuffer)
+from .layout import band_rows, owned_pixels
+
+__all__ = [n for n in dir() if not n.startswith("_")]

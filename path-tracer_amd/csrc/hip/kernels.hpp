@@ -1,0 +1,55 @@
+// kernels.hpp — launch interface between runtime.cpp and kernels.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../../include/pt_packed.h"
+
+// Traversal-stack entries kept in LDS per thread (TLAS + BLAS combined);
+// deeper entries go to a per-slot global spill area (only allocated when the
+// scene's BVH depths need it).
+#ifndef PT_LDS_STACK
+#define PT_LDS_STACK 16
+#endif
+
+namespace ptd {
+
+struct dscene;
+
+// Per-slot state, SoA of 16-byte records.
+struct dslots {
+    float4* ray;        // origin.xyz, packed velocity
+    float4* hit;        // time, shape<<16|material, packed normal, packed tangent
+    float2* uv;
+    float4* thr;        // throughput[4]
+    float4* prob;       // probability[4]
+    float4* smp;        // sample.xyz, normalized lambda0
+    uint2* act;         // active-shape stack (2 x u16 pairs)
+    uint32_t* spill;    // traversal stack spill, (64 - PT_LDS_STACK) x n
+    uint32_t n;
+};
+
+struct dframe {
+    float4* accum;      // width x height, XYZ sum + count
+    uint32_t width, height;
+    uint32_t rank, nranks;
+    uint32_t tiles_x;
+};
+
+struct dparams {
+    uint32_t camera_index;
+    uint32_t render_flags;
+    float termination_probability;
+    uint32_t seed;
+};
+
+}  // namespace ptd
+
+hipError_t pt_launch_raygen(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
+                            hipStream_t st);
+hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, bool spill,
+                            hipStream_t st);
+hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
+                           hipStream_t st);
+hipError_t pt_launch_trace_rays(const ptd::dscene& S, uint32_t n, const float* origins, const uint32_t* vel,
+                                const float* dur, float4* rec, float2* uv, uint32_t* spill, hipStream_t st);

@@ -1,0 +1,363 @@
+// pt_device.hpp — device-side integrator functions for gfx950.
+//
+// GPU restatement of the reference's device code (src/scene/scene.glsl.inc,
+// src/scene/basic_*.glsl.inc, src/core/common.glsl.inc,
+// src/core/spectrum.glsl.inc, src/integrator/basic_scatter.glsl) under the
+// numerics convention of include/pt_fp.h.  Scene data is read through
+// 16-byte vector loads; the traversal stack lives in LDS with a global
+// spill area for depth beyond PT_LDS_STACK (see extend kernel).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include "../../../include/pt_glsl.h"
+#include "../../../include/pt_packed.h"
+
+#define PT_DEV __device__ __forceinline__
+
+namespace ptd {
+
+constexpr uint32_t SHAPE_INDEX_NONE = 0xFFFFFFFFu;
+constexpr uint32_t TEXTURE_INDEX_NONE = 0xFFFFFFFFu;
+
+// Device view of the packed scene (the 11 descriptor bindings of
+// scene.glsl.inc:121-179).
+struct dscene {
+    pt_packed_scene_globals g;
+    const pt_packed_texture* textures;
+    const uint32_t* material;
+    const pt_packed_shape* shapes;
+    const float4* shape_nodes;     // 2 x float4 per node
+    const float4* mesh_faces;      // 3 x float4 per face
+    const uint2* mesh_vertices;
+    const float4* mesh_nodes;      // 2 x float4 per node
+    const pt_packed_camera* cameras;
+    const float4* atlas;
+    uint32_t atlas_w, atlas_h, atlas_layers;
+};
+
+struct ray { pt3 Origin; pt3 Velocity; float Duration; };
+struct medium { uint32_t Priority; pt4 IOR, AbsorptionRate, ScatteringRate; float ScatteringAnisotropy; };
+
+PT_DEV pt3 xyz(float4 a) { return v3(a.x, a.y, a.z); }
+
+// --- common.glsl.inc ------------------------------------------------------
+
+PT_DEV pt3 TransformNormal(pt3 N, const float* From) { return normalize(vec_mul_mat4(N, From)); }
+PT_DEV pt3 TransformDirection(pt3 D, const float* To) { return normalize(mat4_mul_vector(To, D)); }
+
+PT_DEV pt3 SafeNormalize(pt3 V)
+{
+    float LenSq = dot(V, V);
+    if (LenSq < 1e-12f) return v3(0, 0, 1);
+    return V / pt_sqrt(LenSq);
+}
+
+PT_DEV pt3 ComputeTangentVector(pt3 N)
+{
+    pt3 V = pt_abs(N.x) < 0.9f ? v3(1, 0, 0) : v3(0, 1, 0);
+    return normalize(cross(V, N));
+}
+
+PT_DEV void ComputeCoordinateFrame(pt3 Z, pt3& X, pt3& Y)
+{
+    pt3 V = pt_abs(Z.x) < 0.9f ? v3(1, 0, 0) : v3(0, 1, 0);
+    X = normalize(cross(V, Z));
+    Y = cross(X, Z);
+}
+
+PT_DEV uint32_t PackUnitVector(pt3 V)
+{
+    float s = 1.0f / (pt_abs(V.x) + pt_abs(V.y) + pt_abs(V.z));
+    float Px = V.x * s, Py = V.y * s;
+    if (V.z <= 0.0f) {
+        float Sx = Px >= 0.0f ? 1.0f : -1.0f, Sy = Py >= 0.0f ? 1.0f : -1.0f;
+        float Nx = (1.0f - pt_abs(Py)) * Sx;
+        float Ny = (1.0f - pt_abs(Px)) * Sy;
+        Px = Nx; Py = Ny;
+    }
+    return pt_pack_snorm16(Px) | (pt_pack_snorm16(Py) << 16);
+}
+
+PT_DEV pt3 UnpackUnitVector(uint32_t P)
+{
+    float Px = pt_unpack_snorm16(P & 0xFFFFu), Py = pt_unpack_snorm16(P >> 16);
+    float Z = 1.0f - pt_abs(Px) - pt_abs(Py);
+    if (Z < 0.0f) {
+        float Sx = Px >= 0.0f ? 1.0f : -1.0f, Sy = Py >= 0.0f ? 1.0f : -1.0f;
+        float Nx = (1.0f - pt_abs(Py)) * Sx;
+        float Ny = (1.0f - pt_abs(Px)) * Sy;
+        Px = Nx; Py = Ny;
+    }
+    return normalize(v3(Px, Py, Z));
+}
+
+// Slab test (common.glsl.inc:153-185) with true division.
+PT_DEV float IntersectBoundingBox(pt3 O, pt3 V, float Reach, float4 MinAndX, float4 MaxAndX)
+{
+    pt3 MinT = (xyz(MinAndX) - O) / V;
+    pt3 MaxT = (xyz(MaxAndX) - O) / V;
+    float Ex = pt_min(MinT.x, MaxT.x), Ey = pt_min(MinT.y, MaxT.y), Ez = pt_min(MinT.z, MaxT.z);
+    float Lx = pt_max(MinT.x, MaxT.x), Ly = pt_max(MinT.y, MaxT.y), Lz = pt_max(MinT.z, MaxT.z);
+    float EntryT = pt_max(pt_max(Ex, Ey), Ez);
+    float ExitT = pt_min(pt_min(Lx, Ly), Lz);
+    if (ExitT < EntryT) return PT_INFINITY;
+    if (ExitT <= 0) return PT_INFINITY;
+    if (EntryT >= Reach) return PT_INFINITY;
+    return EntryT;
+}
+
+struct rng {
+    uint32_t State;
+    PT_DEV float R01() { return pt_random01(&State); }
+};
+
+PT_DEV pt2 RandomPointOnDisk(rng& G)
+{
+    float R = pt_sqrt(G.R01());
+    float Theta = G.R01() * PT_TAU;
+    return R * v2(pt_cos(Theta), pt_sin(Theta));
+}
+
+PT_DEV pt3 RandomDirection(rng& G)
+{
+    float Z = 2 * G.R01() - 1;
+    float R = pt_sqrt(1 - Z * Z);
+    float Phi = PT_TAU * G.R01();
+    return v3(R * pt_cos(Phi), R * pt_sin(Phi), Z);
+}
+
+PT_DEV pt3 RandomVonMisesFisher(rng& G, float Kappa, pt3 Mu)
+{
+    float Xi = G.R01();
+    float Z = 1 + (1 / Kappa) * pt_log(Xi + (1 - Xi) * pt_exp(-2 * Kappa));
+    float R = pt_sqrt(1 - Z * Z);
+    float Phi = G.R01() * PT_TAU;
+    pt3 V = v3(R * pt_cos(Phi), R * pt_sin(Phi), Z);
+    pt3 MuX, MuY;
+    ComputeCoordinateFrame(Mu, MuX, MuY);
+    return SafeNormalize(V.x * MuX + V.y * MuY + V.z * Mu);
+}
+
+PT_DEV float VonMisesFisherPDF(float Kappa, pt3 Mu, pt3 Direction)
+{
+    if (Kappa < PT_EPSILON) return 1.0f / (4 * PT_PI);
+    float C = Kappa / (2 * PT_PI * (1 - pt_exp(-2 * Kappa)));
+    return C * pt_exp(Kappa * (dot(Mu, Direction) - 1.0f));
+}
+
+PT_DEV pt3 SampleDirectionHG(float Anisotropy, float U1, float U2)
+{
+    float Z;
+    if (pt_abs(Anisotropy) < 1e-3f) {
+        Z = 1 - 2 * U1;
+    } else {
+        float G = Anisotropy;
+        float S = (1 - G * G) / (1 + G - 2 * G * U1);
+        Z = -(1 + G * G - S * S) / (2 * G);
+    }
+    float R = pt_sqrt(1 - Z * Z);
+    float Phi = U2 * PT_TAU;
+    return v3(R * pt_cos(Phi), R * pt_sin(Phi), Z);
+}
+
+PT_DEV pt2 GGXRoughnessAlpha(float Roughness, float Anisotropy)
+{
+    float R = Roughness;
+    float S = 1 - Anisotropy;
+    float AlphaX = R * R * pt_sqrt(2 / (1 + S * S));
+    return v2(AlphaX, S * AlphaX);
+}
+
+PT_DEV float GGXSmithG1(pt3 D, pt2 A)
+{
+    pt3 DSq = D * D;
+    if (DSq.z < PT_EPSILON) return 0.0f;
+    pt2 ASq = A * A;
+    float T = dot(ASq, v2(DSq.x, DSq.y)) / DSq.z;
+    return 2.0f / (1.0f + pt_sqrt(1.0f + T));
+}
+
+PT_DEV pt3 GGXVisibleNormal(pt3 D, pt2 A, float U1, float U2)
+{
+    pt3 Vz = SafeNormalize(v3(A.x * D.x, A.y * D.y, D.z));
+    float LengthSq = dot(v2(Vz.x, Vz.y), v2(Vz.x, Vz.y));
+    pt3 Vx = LengthSq > 0 ? v3(-Vz.y, Vz.x, 0) / pt_sqrt(LengthSq) : v3(1, 0, 0);
+    pt3 Vy = cross(Vz, Vx);
+    float R = pt_sqrt(U1);
+    float Phi = PT_TAU * U2;
+    float S = 0.5f * (1.0f + Vz.z);
+    float Tx = R * pt_cos(Phi);
+    float Ty = (1.0f - S) * pt_sqrt(1.0f - Tx * Tx) + S * R * pt_sin(Phi);
+    float Tz = pt_sqrt(pt_max(0.0f, 1.0f - Tx * Tx - Ty * Ty));
+    pt3 N = Tx * Vx + Ty * Vy + Tz * Vz;
+    return SafeNormalize(v3(A.x * N.x, A.y * N.y, pt_max(0.0f, N.z)));
+}
+
+PT_DEV float GGXDistribution(pt3 N, pt2 A)
+{
+    pt2 I = v2(1.0f / A.x, 1.0f / A.y);
+    float B = dot(N * N, v3(I.x * I.x, I.y * I.y, 1.0f));
+    return 1.0f / (PT_PI * A.x * A.y * B * B);
+}
+
+PT_DEV pt4 CauchyEmpiricalIOR(float BaseIOR, float AbbeNumber, pt4 Lambda)
+{
+    const float LC = 656.3f, Ld = 587.6f, LF = 486.1f;
+    float B = (BaseIOR - 1) / (AbbeNumber * (1.0f / (LF * LF) - 1.0f / (LC * LC)));
+    float A = BaseIOR - B / (Ld * Ld);
+    return A + B / (Lambda * Lambda);
+}
+
+PT_DEV float ComputeCosThetaRefracted(float Eta, float CosTheta)
+{
+    float C2 = 1 - Eta * Eta * (1 - CosTheta * CosTheta);
+    return -pt_sign(CosTheta) * pt_sqrt(pt_max(C2, 0.0f));
+}
+
+PT_DEV pt4 ComputeCosThetaRefracted(pt4 Eta, pt4 CosTheta)
+{
+    pt4 C2 = 1 - Eta * Eta * (1 - CosTheta * CosTheta);
+    return -vsign(CosTheta) * vsqrt(vmax(C2, 0.0f));
+}
+
+PT_DEV float FresnelDielectric(float Eta, float C1, float C2)
+{
+    float Ks = Eta * C1;
+    float Rs = (Ks + C2) / (Ks - C2);
+    float Kp = Eta * C2;
+    float Rp = (Kp + C1) / (Kp - C1);
+    return 0.5f * (Rs * Rs + Rp * Rp);
+}
+
+PT_DEV pt4 FresnelDielectric(pt4 Eta, pt4 C1, pt4 C2)
+{
+    pt4 Ks = Eta * C1;
+    pt4 Rs = (Ks + C2) / (Ks - C2);
+    pt4 Kp = Eta * C2;
+    pt4 Rp = (Kp + C1) / (Kp - C1);
+    return 0.5f * (Rs * Rs + Rp * Rp);
+}
+
+PT_DEV pt4 FresnelDielectric(pt4 Eta, pt4 C1) { return FresnelDielectric(Eta, C1, ComputeCosThetaRefracted(Eta, C1)); }
+
+PT_DEV float Pow5(float x) { float x2 = x * x; return (x2 * x2) * x; }
+PT_DEV float Pow6(float x) { float x2 = x * x; return (x2 * x2) * x2; }
+
+PT_DEV pt4 SchlickFresnelMetal(pt4 Base, pt4 Specular, float CosTheta)
+{
+    const float CosThetaMax = 1 / 7.0f;
+    pt4 FSchlick = Base + (1 - Base) * Pow5(1.0f - CosTheta);
+    pt4 FSchlickMax = Base + (1 - Base) * Pow5(1 - CosThetaMax);
+    pt4 FMax = Specular * FSchlickMax;
+    const float Denominator = CosThetaMax * Pow6(1 - CosThetaMax);
+    float Nominator = CosTheta * Pow6(1.0f - CosTheta);
+    return FSchlick - (Nominator / Denominator) * (FSchlickMax - FMax);
+}
+
+// --- spectrum.glsl.inc ----------------------------------------------------
+
+PT_DEV pt3 SampleStandardObserver(float L)
+{
+    pt3 R;
+    {
+        float T1 = (L - 442.0f) * (L < 442.0f ? 0.0624f : 0.0374f);
+        float T2 = (L - 599.8f) * (L < 599.8f ? 0.0264f : 0.0323f);
+        float T3 = (L - 501.1f) * (L < 501.1f ? 0.0490f : 0.0382f);
+        R.x = 0.362f * pt_exp(-0.5f * T1 * T1) + 1.056f * pt_exp(-0.5f * T2 * T2) - 0.065f * pt_exp(-0.5f * T3 * T3);
+    }
+    {
+        float T1 = (L - 568.8f) * (L < 568.8f ? 0.0213f : 0.0247f);
+        float T2 = (L - 530.9f) * (L < 530.9f ? 0.0613f : 0.0322f);
+        R.y = 0.821f * pt_exp(-0.5f * T1 * T1) + 0.286f * pt_exp(-0.5f * T2 * T2);
+    }
+    {
+        float T1 = (L - 437.0f) * (L < 437.0f ? 0.0845f : 0.0278f);
+        float T2 = (L - 459.0f) * (L < 459.0f ? 0.0385f : 0.0725f);
+        R.z = 1.217f * pt_exp(-0.5f * T1 * T1) + 0.681f * pt_exp(-0.5f * T2 * T2);
+    }
+    return R;
+}
+
+PT_DEV float SampleParametricSpectrum(pt3 B, float L)
+{
+    float X = (B.x * L + B.y) * L + B.z;
+    return 0.5f + X / (2.0f * pt_sqrt(1.0f + X * X));
+}
+
+PT_DEV pt4 SampleParametricSpectrum(pt3 B, pt4 L)
+{
+    return v4(SampleParametricSpectrum(B, L.x), SampleParametricSpectrum(B, L.y), SampleParametricSpectrum(B, L.z),
+              SampleParametricSpectrum(B, L.w));
+}
+
+// --- scene data access ----------------------------------------------------
+
+PT_DEV float4 Texel(const dscene& S, uint32_t Layer, int X, int Y)
+{
+    int W = (int)S.atlas_w, H = (int)S.atlas_h;
+    X %= W; if (X < 0) X += W;
+    Y %= H; if (Y < 0) Y += H;
+    if (S.atlas_layers == 0) return make_float4(0, 0, 0, 0);
+    if (Layer >= S.atlas_layers) Layer = S.atlas_layers - 1;
+    return S.atlas[((size_t)Layer * H + Y) * W + X];
+}
+
+PT_DEV pt4 f4(float4 a) { return v4(a.x, a.y, a.z, a.w); }
+
+// SampleTexture (scene.glsl.inc:181-205) with software REPEAT filtering.
+PT_DEV pt4 SampleTexture(const dscene& S, uint32_t Index, pt2 UV)
+{
+    const pt_packed_texture T = S.textures[Index];
+    float U = pt_mix(T.AtlasPlacementMinimum[0], T.AtlasPlacementMaximum[0], pt_fract(UV.x));
+    float V = pt_mix(T.AtlasPlacementMinimum[1], T.AtlasPlacementMaximum[1], pt_fract(UV.y));
+    float W = (float)S.atlas_w, H = (float)S.atlas_h;
+    if (T.Flags & PT_TEXTURE_FLAG_FILTER_NEAREST)
+        return f4(Texel(S, T.AtlasImageIndex, (int)pt_floor(U * W), (int)pt_floor(V * H)));
+    float Us = U * W - 0.5f, Vs = V * H - 0.5f;
+    float Fi = pt_floor(Us), Fj = pt_floor(Vs);
+    float A = Us - Fi, B = Vs - Fj;
+    int I0 = (int)Fi, J0 = (int)Fj;
+    pt4 T00 = f4(Texel(S, T.AtlasImageIndex, I0, J0)), T10 = f4(Texel(S, T.AtlasImageIndex, I0 + 1, J0));
+    pt4 T01 = f4(Texel(S, T.AtlasImageIndex, I0, J0 + 1)), T11 = f4(Texel(S, T.AtlasImageIndex, I0 + 1, J0 + 1));
+    return ((1 - A) * (1 - B)) * T00 + (A * (1 - B)) * T10 + ((1 - A) * B) * T01 + (A * B) * T11;
+}
+
+PT_DEV pt4 SampleSkyboxRadiance(const dscene& S, pt3 D, pt4 Lambda)
+{
+    pt4 Spectrum;
+    if (S.g.SkyboxTextureIndex == TEXTURE_INDEX_NONE) {
+        Spectrum = v4(0, 0, 100, 1);
+    } else {
+        float Phi = pt_atan2(D.y, D.x);
+        float Theta = pt_asin(D.z);
+        float U = 0.5f + Phi / PT_TAU;
+        float V = 0.5f + Theta / PT_PI;
+        Spectrum = SampleTexture(S, S.g.SkyboxTextureIndex, v2(U, V));
+    }
+    return (Spectrum.w * SampleParametricSpectrum(v3(Spectrum.x, Spectrum.y, Spectrum.z), Lambda)) * S.g.SkyboxBrightness;
+}
+
+PT_DEV uint32_t MUint(const dscene& S, uint32_t M, uint32_t A) { return S.material[32 * M + A]; }
+PT_DEV float MFloat(const dscene& S, uint32_t M, uint32_t A) { return pt_u2f(MUint(S, M, A)); }
+PT_DEV pt3 MVec3(const dscene& S, uint32_t M, uint32_t A) { return v3(MFloat(S, M, A), MFloat(S, M, A + 1), MFloat(S, M, A + 2)); }
+
+PT_DEV pt4 MaterialTexturableReflectance(const dscene& S, uint32_t M, uint32_t A, pt4 Lambda, pt2 UV)
+{
+    pt4 Value = SampleParametricSpectrum(MVec3(S, M, A), Lambda);
+    uint32_t Tx = MUint(S, M, A + 3);
+    if (Tx != TEXTURE_INDEX_NONE) {
+        pt4 T = SampleTexture(S, Tx, UV);
+        Value = Value * SampleParametricSpectrum(v3(T.x, T.y, T.z), Lambda);
+    }
+    return Value;
+}
+
+PT_DEV float MaterialTexturableValue(const dscene& S, uint32_t M, uint32_t A, pt2 UV)
+{
+    float Value = MFloat(S, M, A);
+    uint32_t Tx = MUint(S, M, A + 1);
+    if (Tx != TEXTURE_INDEX_NONE) Value *= SampleTexture(S, Tx, UV).x;
+    return Value;
+}
+
+}  // namespace ptd

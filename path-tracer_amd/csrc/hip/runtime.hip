@@ -1,0 +1,725 @@
+// runtime.hip — host side of libpathtracer.so: the C ABI of include/pt_api.h.
+//
+// Replaces the reference's Vulkan integrator host (src/integrator/basic.cpp,
+// src/integrator/integrator.cpp:15-87) and scene upload
+// (src/scene/scene.cpp:1643-2006) with HIP: device buffers for the packed
+// scene, a float4 sample buffer, SoA slot buffers, and kernel launches on one
+// stream per device.  Scene packs are validated on the host before upload so
+// that no index in them can send a kernel out of bounds or into a cycle.
+#include "pt_device.hpp"
+#include "kernels.hpp"
+#include "../../../include/pt_api.h"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_last_error;
+
+void SetError(const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+}
+
+#define PT_HIP(call)                                                                         \
+    do {                                                                                     \
+        hipError_t e_ = (call);                                                              \
+        if (e_ != hipSuccess) {                                                              \
+            SetError("%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, __LINE__); \
+            return (int)e_;                                                                  \
+        }                                                                                    \
+    } while (0)
+
+template <class T>
+struct dbuf {
+    T* ptr = nullptr;
+    size_t count = 0;
+    void release() { if (ptr) (void)hipFree(ptr); ptr = nullptr; count = 0; }
+    hipError_t upload(const T* src, size_t n)
+    {
+        if (n > count) {
+            release();
+            hipError_t e = hipMalloc(&ptr, std::max<size_t>(n, 1) * sizeof(T));
+            if (e != hipSuccess) { ptr = nullptr; return e; }
+            count = n;
+        }
+        if (n == 0) return hipSuccess;
+        return hipMemcpy(ptr, src, n * sizeof(T), hipMemcpyHostToDevice);
+    }
+    hipError_t alloc(size_t n)
+    {
+        if (n <= count && ptr) return hipSuccess;
+        release();
+        hipError_t e = hipMalloc(&ptr, std::max<size_t>(n, 1) * sizeof(T));
+        if (e != hipSuccess) { ptr = nullptr; return e; }
+        count = n;
+        return hipSuccess;
+    }
+};
+
+struct event_pair { hipEvent_t a, b; int kernel; };
+
+}  // namespace
+
+struct pt_device {
+    int id = 0;
+    hipStream_t stream = nullptr;
+    bool profiling = false;
+    std::vector<event_pair> pending;
+    std::vector<event_pair> free_events;
+    uint64_t launches[PT_KERNEL_COUNT] = {};
+    double total_ms[PT_KERNEL_COUNT] = {};
+};
+
+struct pt_scene {
+    pt_device* dev = nullptr;
+    ptd::dscene d{};
+    dbuf<pt_packed_texture> textures;
+    dbuf<uint32_t> material;
+    dbuf<pt_packed_shape> shapes;
+    dbuf<pt_packed_shape_node> shape_nodes;
+    dbuf<pt_packed_mesh_face> faces;
+    dbuf<pt_packed_mesh_vertex> vertices;
+    dbuf<pt_packed_mesh_node> mesh_nodes;
+    dbuf<pt_packed_camera> cameras;
+    dbuf<float> atlas;
+    uint32_t camera_count = 0;
+    uint32_t stack_needed = 0;   // max traversal stack entries (TLAS + BLAS)
+    bool valid = false;
+};
+
+struct pt_sample_buffer {
+    pt_device* dev = nullptr;
+    uint32_t width = 0, height = 0;
+    float4* accum = nullptr;
+};
+
+struct pt_basic_renderer {
+    pt_basic_renderer_params params{};
+    pt_device* dev = nullptr;
+    pt_scene* scene = nullptr;          // non-owning (basic.hpp:8,21)
+    pt_sample_buffer* buffer = nullptr; // non-owning
+    uint32_t rank = 0, nranks = 1;
+    uint32_t tiles_x = 0;
+    ptd::dslots slots{};
+    dbuf<float4> ray, hit, thr, prob, smp;
+    dbuf<float2> uv;
+    dbuf<uint2> act;
+    dbuf<uint32_t> spill;
+};
+
+struct pt_comm {
+    pt_device* dev = nullptr;
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+};
+
+namespace {
+
+int BeginTimed(pt_device* dev, int kernel, event_pair& ep)
+{
+    if (!dev->profiling) return 0;
+    if (!dev->free_events.empty()) { ep = dev->free_events.back(); dev->free_events.pop_back(); }
+    else {
+        PT_HIP(hipEventCreate(&ep.a));
+        PT_HIP(hipEventCreate(&ep.b));
+    }
+    ep.kernel = kernel;
+    PT_HIP(hipEventRecord(ep.a, dev->stream));
+    return 0;
+}
+
+int EndTimed(pt_device* dev, event_pair& ep)
+{
+    if (!dev->profiling) return 0;
+    PT_HIP(hipEventRecord(ep.b, dev->stream));
+    dev->pending.push_back(ep);
+    return 0;
+}
+
+int CollectTimes(pt_device* dev)
+{
+    if (dev->pending.empty()) return 0;
+    PT_HIP(hipStreamSynchronize(dev->stream));
+    for (event_pair& ep : dev->pending) {
+        float ms = 0;
+        PT_HIP(hipEventElapsedTime(&ms, ep.a, ep.b));
+        dev->launches[ep.kernel] += 1;
+        dev->total_ms[ep.kernel] += ms;
+        dev->free_events.push_back(ep);
+    }
+    dev->pending.clear();
+    return 0;
+}
+
+// --- pack validation --------------------------------------------------------------
+
+bool TexOk(uint32_t t, uint32_t n) { return t == PT_TEXTURE_INDEX_NONE || t < n; }
+
+// Depth (edges on the longest root-leaf path) of the TLAS, or -1 if malformed.
+int TlasDepth(const pt_scene_packs* p)
+{
+    uint32_t n = p->shape_node_count;
+    struct item { uint32_t node, depth; };
+    std::vector<item> st{{0, 0}};
+    int maxd = 0;
+    size_t visits = 0;
+    while (!st.empty()) {
+        item it = st.back(); st.pop_back();
+        if (++visits > (size_t)n) return -1;   // cycle or shared children
+        const pt_packed_shape_node& N = p->shape_nodes[it.node];
+        maxd = std::max<int>(maxd, (int)it.depth);
+        if (N.ChildNodeIndices == 0) {
+            if (N.ShapeIndex >= p->shape_count) return -1;
+        } else {
+            uint32_t a = N.ChildNodeIndices & 0xFFFF, b = N.ChildNodeIndices >> 16;
+            if (a >= n || b >= n) return -1;
+            st.push_back({a, it.depth + 1});
+            st.push_back({b, it.depth + 1});
+        }
+    }
+    return maxd;
+}
+
+int BlasDepth(const pt_scene_packs* p, uint32_t root)
+{
+    uint32_t n = p->mesh_node_count;
+    if (root >= n) return -1;
+    struct item { uint32_t node, depth; };
+    std::vector<item> st{{root, 0}};
+    int maxd = 0;
+    size_t visits = 0;
+    while (!st.empty()) {
+        item it = st.back(); st.pop_back();
+        if (++visits > (size_t)n) return -1;
+        const pt_packed_mesh_node& N = p->mesh_nodes[it.node];
+        maxd = std::max<int>(maxd, (int)it.depth);
+        if (N.FaceEndIndex > 0) {
+            if (N.FaceBeginOrNodeIndex > N.FaceEndIndex || N.FaceEndIndex > p->mesh_face_count) return -1;
+        } else {
+            uint32_t c = N.FaceBeginOrNodeIndex;
+            if (c + 1 >= n || c + 1 < c) return -1;
+            st.push_back({c, it.depth + 1});
+            st.push_back({c + 1, it.depth + 1});
+        }
+    }
+    return maxd;
+}
+
+bool MaterialOk(const pt_scene_packs* p, uint32_t m)
+{
+    if ((uint64_t)m * 32 + 32 > p->material_word_count) return false;
+    const uint32_t* A = p->material_data + 32 * m;
+    uint32_t nt = p->texture_count;
+    switch (A[0]) {
+        case PT_MATERIAL_TYPE_BASIC_DIFFUSE: return TexOk(A[PT_BASIC_DIFFUSE_BASE_SPECTRUM + 3], nt);
+        case PT_MATERIAL_TYPE_BASIC_METAL:
+            return TexOk(A[PT_BASIC_METAL_BASE_SPECTRUM + 3], nt) && TexOk(A[PT_BASIC_METAL_SPECULAR_SPECTRUM + 3], nt) &&
+                   TexOk(A[PT_BASIC_METAL_ROUGHNESS + 1], nt) && TexOk(A[PT_BASIC_METAL_ROUGHNESS_ANISOTROPY + 1], nt);
+        case PT_MATERIAL_TYPE_BASIC_TRANSLUCENT:
+            return TexOk(A[PT_BASIC_TRANSLUCENT_ROUGHNESS + 1], nt) && TexOk(A[PT_BASIC_TRANSLUCENT_ROUGHNESS_ANISOTROPY + 1], nt);
+        default: return true;   // not shaded by the integrator
+    }
+}
+
+int ValidatePacks(const pt_scene_packs* p, uint32_t* stack_needed)
+{
+    if (!p || !p->globals) { SetError("packs: globals missing"); return -1; }
+    const pt_packed_scene_globals& g = *p->globals;
+    if (g.ShapeCount != 0) {
+        if (g.ShapeCount != p->shape_count) { SetError("packs: ShapeCount %u != shape_count %u", g.ShapeCount, p->shape_count); return -1; }
+        if (p->shape_node_count == 0) { SetError("packs: no shape nodes"); return -1; }
+    }
+    if (!TexOk(g.SkyboxTextureIndex, p->texture_count)) { SetError("packs: bad skybox texture"); return -1; }
+    if (p->texture_count > 0 && (!p->atlas || p->atlas_layer_count == 0 || p->atlas_width == 0 || p->atlas_height == 0)) {
+        SetError("packs: textures without atlas"); return -1;
+    }
+    for (uint32_t i = 0; i < p->mesh_face_count; i++) {
+        const pt_packed_mesh_face& F = p->mesh_faces[i];
+        if (F.VertexIndex0 >= p->mesh_vertex_count || F.VertexIndex1 >= p->mesh_vertex_count ||
+            F.VertexIndex2 >= p->mesh_vertex_count) { SetError("packs: face %u vertex out of range", i); return -1; }
+    }
+    int blas = 0;
+    for (uint32_t i = 0; i < p->shape_count; i++) {
+        const pt_packed_shape& S = p->shapes[i];
+        if (S.Type < 0 || S.Type > 3) { SetError("packs: shape %u bad type", i); return -1; }
+        if (!MaterialOk(p, S.MaterialIndex)) { SetError("packs: shape %u bad material %u", i, S.MaterialIndex); return -1; }
+        if (S.Type == PT_SHAPE_TYPE_MESH_INSTANCE) {
+            int d = BlasDepth(p, S.MeshRootNodeIndex);
+            if (d < 0) { SetError("packs: shape %u mesh BVH malformed", i); return -1; }
+            blas = std::max(blas, d);
+        }
+    }
+    int tlas = 0;
+    if (g.ShapeCount != 0) {
+        tlas = TlasDepth(p);
+        if (tlas < 0) { SetError("packs: shape BVH malformed"); return -1; }
+    }
+    *stack_needed = (uint32_t)(std::min(tlas, 32) + std::min(blas, 32));
+    return 0;
+}
+
+ptd::dframe Frame(pt_basic_renderer* r)
+{
+    ptd::dframe F;
+    F.accum = r->buffer->accum;
+    F.width = r->buffer->width;
+    F.height = r->buffer->height;
+    F.rank = r->rank;
+    F.nranks = r->nranks;
+    F.tiles_x = r->tiles_x;
+    return F;
+}
+
+ptd::dparams Params(pt_basic_renderer* r, uint32_t seed)
+{
+    ptd::dparams P;
+    P.camera_index = r->params.CameraIndex;
+    P.render_flags = r->params.RenderFlags;
+    P.termination_probability = r->params.PathTerminationProbability;
+    P.seed = seed;
+    return P;
+}
+
+int EnsureSpill(pt_basic_renderer* r)
+{
+    uint32_t need = r->scene->stack_needed;
+    if (need <= PT_LDS_STACK) { r->slots.spill = nullptr; return 0; }
+    size_t rows = need - PT_LDS_STACK;
+    PT_HIP(r->spill.alloc(rows * (size_t)r->slots.n));
+    r->slots.spill = r->spill.ptr;
+    return 0;
+}
+
+int CheckReady(pt_basic_renderer* r)
+{
+    if (!r || !r->scene || !r->buffer) { SetError("renderer: null"); return -1; }
+    if (!r->scene->valid) { SetError("renderer: scene has no valid packs (call ptUpdateScene)"); return -1; }
+    if (r->params.CameraIndex >= r->scene->camera_count) {
+        SetError("renderer: CameraIndex %u >= camera count %u", r->params.CameraIndex, r->scene->camera_count);
+        return -1;
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ptGetLastError(void) { return g_last_error.c_str(); }
+
+int ptGetDeviceCount(int* count)
+{
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *count = n;
+    return 0;
+}
+
+pt_device* ptCreateDevice(int hip_device)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) { SetError("no HIP device available"); return nullptr; }
+    if (hip_device < 0 || hip_device >= n) { SetError("device %d out of range (%d devices)", hip_device, n); return nullptr; }
+    if (hipSetDevice(hip_device) != hipSuccess) { SetError("hipSetDevice(%d) failed", hip_device); return nullptr; }
+    pt_device* d = new pt_device;
+    d->id = hip_device;
+    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
+        SetError("hipStreamCreate failed");
+        delete d;
+        return nullptr;
+    }
+    return d;
+}
+
+void ptDestroyDevice(pt_device* d)
+{
+    if (!d) return;
+    (void)hipSetDevice(d->id);
+    (void)hipStreamSynchronize(d->stream);
+    for (auto& ep : d->pending) { (void)hipEventDestroy(ep.a); (void)hipEventDestroy(ep.b); }
+    for (auto& ep : d->free_events) { (void)hipEventDestroy(ep.a); (void)hipEventDestroy(ep.b); }
+    (void)hipStreamDestroy(d->stream);
+    delete d;
+}
+
+int ptSynchronize(pt_device* d)
+{
+    if (!d) { SetError("null device"); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    PT_HIP(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+pt_scene* ptCreateScene(pt_device* d)
+{
+    if (!d) { SetError("null device"); return nullptr; }
+    pt_scene* s = new pt_scene;
+    s->dev = d;
+    return s;
+}
+
+void ptDestroyScene(pt_device* d, pt_scene* s)
+{
+    if (!s) return;
+    if (d) (void)hipSetDevice(d->id);
+    s->textures.release(); s->material.release(); s->shapes.release(); s->shape_nodes.release();
+    s->faces.release(); s->vertices.release(); s->mesh_nodes.release(); s->cameras.release(); s->atlas.release();
+    delete s;
+}
+
+// UpdateVulkanScene (scene.cpp:1692-2006): synchronous upload of the packs.
+int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t dirty)
+{
+    if (!d || !s) { SetError("null device/scene"); return -1; }
+    uint32_t need = 0;
+    if (ValidatePacks(p, &need) != 0) { s->valid = false; return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    PT_HIP(hipStreamSynchronize(d->stream));   // like vkDeviceWaitIdle (scene.cpp:1704)
+    bool first = !s->valid;
+    if (first || (dirty & PT_SCENE_DIRTY_TEXTURES)) {
+        PT_HIP(s->textures.upload(p->textures, p->texture_count));
+        size_t atlas_floats = (size_t)p->atlas_width * p->atlas_height * 4 * p->atlas_layer_count;
+        PT_HIP(s->atlas.upload(p->atlas, p->atlas ? atlas_floats : 0));
+    }
+    if (first || (dirty & PT_SCENE_DIRTY_MATERIALS)) PT_HIP(s->material.upload(p->material_data, p->material_word_count));
+    if (first || (dirty & PT_SCENE_DIRTY_SHAPES)) {
+        PT_HIP(s->shapes.upload(p->shapes, p->shape_count));
+        PT_HIP(s->shape_nodes.upload(p->shape_nodes, p->shape_node_count));
+    }
+    if (first || (dirty & PT_SCENE_DIRTY_MESHES)) {
+        PT_HIP(s->faces.upload(p->mesh_faces, p->mesh_face_count));
+        PT_HIP(s->vertices.upload(p->mesh_vertices, p->mesh_vertex_count));
+        PT_HIP(s->mesh_nodes.upload(p->mesh_nodes, p->mesh_node_count));
+    }
+    if (first || (dirty & PT_SCENE_DIRTY_CAMERAS)) PT_HIP(s->cameras.upload(p->cameras, p->camera_count));
+
+    ptd::dscene& D = s->d;
+    D.g = *p->globals;
+    D.textures = s->textures.ptr;
+    D.material = s->material.ptr;
+    D.shapes = s->shapes.ptr;
+    D.shape_nodes = reinterpret_cast<const float4*>(s->shape_nodes.ptr);
+    D.mesh_faces = reinterpret_cast<const float4*>(s->faces.ptr);
+    D.mesh_vertices = reinterpret_cast<const uint2*>(s->vertices.ptr);
+    D.mesh_nodes = reinterpret_cast<const float4*>(s->mesh_nodes.ptr);
+    D.cameras = s->cameras.ptr;
+    D.atlas = reinterpret_cast<const float4*>(s->atlas.ptr);
+    D.atlas_w = p->atlas_width;
+    D.atlas_h = p->atlas_height;
+    D.atlas_layers = p->atlas ? p->atlas_layer_count : 0;
+    s->camera_count = p->camera_count;
+    s->stack_needed = need;
+    s->valid = true;
+    return 0;
+}
+
+pt_sample_buffer* ptCreateSampleBuffer(pt_device* d, uint32_t w, uint32_t h)
+{
+    if (!d || w == 0 || h == 0) { SetError("bad sample buffer arguments"); return nullptr; }
+    if (hipSetDevice(d->id) != hipSuccess) { SetError("hipSetDevice failed"); return nullptr; }
+    pt_sample_buffer* b = new pt_sample_buffer;
+    b->dev = d;
+    b->width = w;
+    b->height = h;
+    size_t bytes = (size_t)w * h * sizeof(float4);
+    if (hipMalloc(&b->accum, bytes) != hipSuccess || hipMemset(b->accum, 0, bytes) != hipSuccess) {
+        SetError("sample buffer allocation failed (%zu bytes)", bytes);
+        if (b->accum) (void)hipFree(b->accum);
+        delete b;
+        return nullptr;
+    }
+    return b;
+}
+
+void ptDestroySampleBuffer(pt_device* d, pt_sample_buffer* b)
+{
+    if (!b) return;
+    if (d) (void)hipSetDevice(d->id);
+    if (b->accum) (void)hipFree(b->accum);
+    delete b;
+}
+
+int ptReadSampleBuffer(pt_device* d, pt_sample_buffer* b, float* rgba)
+{
+    if (!d || !b || !rgba) { SetError("null argument"); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    PT_HIP(hipMemcpyAsync(rgba, b->accum, (size_t)b->width * b->height * sizeof(float4), hipMemcpyDeviceToHost, d->stream));
+    PT_HIP(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, pt_sample_buffer* b, uint32_t rank,
+                                                    uint32_t nranks)
+{
+    if (!d || !s || !b) { SetError("null argument"); return nullptr; }
+    if (nranks == 0 || rank >= nranks) { SetError("bad partition %u/%u", rank, nranks); return nullptr; }
+    if (hipSetDevice(d->id) != hipSuccess) { SetError("hipSetDevice failed"); return nullptr; }
+    pt_basic_renderer* r = new pt_basic_renderer;
+    r->dev = d;
+    r->scene = s;
+    r->buffer = b;
+    r->rank = rank;
+    r->nranks = nranks;
+    r->tiles_x = (b->width + 15) / 16;
+    uint32_t bands = (b->height + 15) / 16;
+    uint32_t owned = bands > rank ? (bands - rank + nranks - 1) / nranks : 0;
+    uint64_t n = (uint64_t)owned * r->tiles_x * 256;
+    if (n > 0xFFFFFFFFull / 2) { SetError("too many slots"); delete r; return nullptr; }
+    uint32_t ns = (uint32_t)n;
+    bool ok = r->ray.alloc(ns) == hipSuccess && r->hit.alloc(ns) == hipSuccess && r->thr.alloc(ns) == hipSuccess &&
+              r->prob.alloc(ns) == hipSuccess && r->smp.alloc(ns) == hipSuccess && r->uv.alloc(ns) == hipSuccess &&
+              r->act.alloc(ns) == hipSuccess;
+    if (ok && ns) {
+        ok = hipMemset(r->ray.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->hit.ptr, 0, (size_t)ns * 16) == hipSuccess &&
+             hipMemset(r->thr.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->prob.ptr, 0, (size_t)ns * 16) == hipSuccess &&
+             hipMemset(r->smp.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->uv.ptr, 0, (size_t)ns * 8) == hipSuccess &&
+             hipMemset(r->act.ptr, 0, (size_t)ns * 8) == hipSuccess;
+    }
+    if (!ok) {
+        SetError("renderer slot allocation failed (%u slots)", ns);
+        r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->smp.release(); r->uv.release(); r->act.release();
+        delete r;
+        return nullptr;
+    }
+    r->slots.ray = r->ray.ptr;
+    r->slots.hit = r->hit.ptr;
+    r->slots.uv = r->uv.ptr;
+    r->slots.thr = r->thr.ptr;
+    r->slots.prob = r->prob.ptr;
+    r->slots.smp = r->smp.ptr;
+    r->slots.act = r->act.ptr;
+    r->slots.spill = nullptr;
+    r->slots.n = ns;
+    return r;
+}
+
+pt_basic_renderer* ptCreateBasicRenderer(pt_device* d, pt_scene* s, pt_sample_buffer* b)
+{
+    return ptCreateBasicRendererPartitioned(d, s, b, 0, 1);
+}
+
+void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
+{
+    if (!r) return;
+    if (d) { (void)hipSetDevice(d->id); (void)hipStreamSynchronize(d->stream); }
+    r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->smp.release();
+    r->uv.release(); r->act.release(); r->spill.release();
+    delete r;
+}
+
+pt_basic_renderer_params* ptBasicRendererParams(pt_basic_renderer* r) { return r ? &r->params : nullptr; }
+uint32_t ptBasicRendererSlotCount(pt_basic_renderer* r) { return r ? r->slots.n : 0; }
+
+// ResetBasicRenderer (basic.cpp:285-304)
+int ptResetBasicRenderer(pt_device* d, pt_basic_renderer* r)
+{
+    if (!d) { SetError("null device"); return -1; }
+    if (CheckReady(r) != 0) return -1;
+    PT_HIP(hipSetDevice(d->id));
+    event_pair ep{};
+    if (int e = BeginTimed(d, PT_KERNEL_RAYGEN, ep)) return e;
+    PT_HIP(pt_launch_raygen(r->scene->d, r->slots, Frame(r), Params(r, r->params.FrameIndex), d->stream));
+    return EndTimed(d, ep);
+}
+
+// RunBasicRenderer (basic.cpp:306-332)
+int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
+{
+    if (!d) { SetError("null device"); return -1; }
+    if (CheckReady(r) != 0) return -1;
+    PT_HIP(hipSetDevice(d->id));
+    if (int e = EnsureSpill(r)) return e;
+    r->params.FrameIndex += 1;
+    ptd::dparams P = Params(r, r->params.FrameIndex);
+    ptd::dframe F = Frame(r);
+    bool spill = r->slots.spill != nullptr;
+    for (uint32_t i = 0; i < rounds; i++) {
+        event_pair ep{};
+        if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep)) return e;
+        PT_HIP(pt_launch_extend(r->scene->d, r->slots, F, spill, d->stream));
+        if (int e = EndTimed(d, ep)) return e;
+        if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep)) return e;
+        PT_HIP(pt_launch_shade(r->scene->d, r->slots, F, P, d->stream));
+        if (int e = EndTimed(d, ep)) return e;
+    }
+    return 0;
+}
+
+int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state* out)
+{
+    if (!d || !r || !out) { SetError("null argument"); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    PT_HIP(hipStreamSynchronize(d->stream));
+    uint32_t n = r->slots.n;
+    std::vector<float4> ray(n), hit(n), thr(n), prob(n), smp(n);
+    std::vector<float2> uv(n);
+    std::vector<uint2> act(n);
+    PT_HIP(hipMemcpy(ray.data(), r->ray.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
+    PT_HIP(hipMemcpy(hit.data(), r->hit.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
+    PT_HIP(hipMemcpy(thr.data(), r->thr.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
+    PT_HIP(hipMemcpy(prob.data(), r->prob.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
+    PT_HIP(hipMemcpy(smp.data(), r->smp.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
+    PT_HIP(hipMemcpy(uv.data(), r->uv.ptr, (size_t)n * 8, hipMemcpyDeviceToHost));
+    PT_HIP(hipMemcpy(act.data(), r->act.ptr, (size_t)n * 8, hipMemcpyDeviceToHost));
+    uint32_t W = r->buffer->width, H = r->buffer->height;
+    auto bits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
+    for (uint32_t s = 0; s < n; s++) {
+        uint32_t t = s >> 8, l = s & 255u, k = t / r->tiles_x, tx = t - k * r->tiles_x;
+        uint32_t x = tx * 16 + (l & 15u), y = (r->rank + k * r->nranks) * 16 + (l >> 4);
+        if (x >= W || y >= H) continue;
+        pt_pixel_state& O = out[(size_t)y * W + x];
+        O.origin[0] = ray[s].x; O.origin[1] = ray[s].y; O.origin[2] = ray[s].z;
+        O.packed_velocity = bits(ray[s].w);
+        O.hit.time = hit[s].x;
+        O.hit.shape_material = bits(hit[s].y);
+        O.hit.packed_normal = bits(hit[s].z);
+        O.hit.packed_tangent = bits(hit[s].w);
+        O.hit.u = uv[s].x;
+        O.hit.v = uv[s].y;
+        O.lambda0 = smp[s].w;
+        O.throughput[0] = thr[s].x; O.throughput[1] = thr[s].y; O.throughput[2] = thr[s].z; O.throughput[3] = thr[s].w;
+        O.probability[0] = prob[s].x; O.probability[1] = prob[s].y; O.probability[2] = prob[s].z; O.probability[3] = prob[s].w;
+        O.sample[0] = smp[s].x; O.sample[1] = smp[s].y; O.sample[2] = smp[s].z;
+        O.active01 = act[s].x;
+        O.active23 = act[s].y;
+    }
+    return 0;
+}
+
+int ptTraceRays(pt_device* d, pt_scene* s, uint32_t n, const float* origins, const uint32_t* vel, const float* dur,
+                pt_hit_record* out)
+{
+    if (!d || !s || (n && (!origins || !vel || !dur || !out))) { SetError("null argument"); return -1; }
+    if (!s->valid) { SetError("scene has no valid packs"); return -1; }
+    if (n == 0) return 0;
+    PT_HIP(hipSetDevice(d->id));
+    float *d_o = nullptr, *d_t = nullptr;
+    uint32_t *d_v = nullptr, *d_spill = nullptr;
+    float4* d_rec = nullptr;
+    float2* d_uv = nullptr;
+    int rc = 0;
+    auto cleanup = [&]() {
+        if (d_o) (void)hipFree(d_o);
+        if (d_t) (void)hipFree(d_t);
+        if (d_v) (void)hipFree(d_v);
+        if (d_spill) (void)hipFree(d_spill);
+        if (d_rec) (void)hipFree(d_rec);
+        if (d_uv) (void)hipFree(d_uv);
+    };
+    do {
+        hipError_t e;
+        if ((e = hipMalloc(&d_o, (size_t)n * 12)) != hipSuccess) { rc = e; break; }
+        if ((e = hipMalloc(&d_t, (size_t)n * 4)) != hipSuccess) { rc = e; break; }
+        if ((e = hipMalloc(&d_v, (size_t)n * 4)) != hipSuccess) { rc = e; break; }
+        if ((e = hipMalloc(&d_rec, (size_t)n * 16)) != hipSuccess) { rc = e; break; }
+        if ((e = hipMalloc(&d_uv, (size_t)n * 8)) != hipSuccess) { rc = e; break; }
+        if (s->stack_needed > PT_LDS_STACK)
+            if ((e = hipMalloc(&d_spill, (size_t)(s->stack_needed - PT_LDS_STACK) * n * 4)) != hipSuccess) { rc = e; break; }
+        if ((e = hipMemcpy(d_o, origins, (size_t)n * 12, hipMemcpyHostToDevice)) != hipSuccess) { rc = e; break; }
+        if ((e = hipMemcpy(d_t, dur, (size_t)n * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = e; break; }
+        if ((e = hipMemcpy(d_v, vel, (size_t)n * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = e; break; }
+        if ((e = pt_launch_trace_rays(s->d, n, d_o, d_v, d_t, d_rec, d_uv, d_spill, d->stream)) != hipSuccess) { rc = e; break; }
+        if ((e = hipStreamSynchronize(d->stream)) != hipSuccess) { rc = e; break; }
+        std::vector<float4> rec(n);
+        std::vector<float2> uv(n);
+        if ((e = hipMemcpy(rec.data(), d_rec, (size_t)n * 16, hipMemcpyDeviceToHost)) != hipSuccess) { rc = e; break; }
+        if ((e = hipMemcpy(uv.data(), d_uv, (size_t)n * 8, hipMemcpyDeviceToHost)) != hipSuccess) { rc = e; break; }
+        for (uint32_t i = 0; i < n; i++) {
+            std::memcpy(&out[i].time, &rec[i].x, 4);
+            std::memcpy(&out[i].shape_material, &rec[i].y, 4);
+            std::memcpy(&out[i].packed_normal, &rec[i].z, 4);
+            std::memcpy(&out[i].packed_tangent, &rec[i].w, 4);
+            out[i].u = uv[i].x;
+            out[i].v = uv[i].y;
+        }
+    } while (0);
+    if (rc) SetError("ptTraceRays: %s", hipGetErrorString((hipError_t)rc));
+    cleanup();
+    return rc;
+}
+
+int ptSetProfiling(pt_device* d, int enable)
+{
+    if (!d) { SetError("null device"); return -1; }
+    if (int e = CollectTimes(d)) return e;
+    d->profiling = enable != 0;
+    return 0;
+}
+
+int ptGetKernelStats(pt_device* d, int kernel, uint64_t* launches, double* total_ms)
+{
+    if (!d || kernel < 0 || kernel >= PT_KERNEL_COUNT) { SetError("bad argument"); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    if (int e = CollectTimes(d)) return e;
+    if (launches) *launches = d->launches[kernel];
+    if (total_ms) *total_ms = d->total_ms[kernel];
+    return 0;
+}
+
+int ptResetKernelStats(pt_device* d)
+{
+    if (!d) { SetError("null device"); return -1; }
+    if (int e = CollectTimes(d)) return e;
+    for (int k = 0; k < PT_KERNEL_COUNT; k++) { d->launches[k] = 0; d->total_ms[k] = 0; }
+    return 0;
+}
+
+// --- RCCL ------------------------------------------------------------------------
+
+int ptCommGetUniqueId(uint8_t id[128])
+{
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId u;
+    ncclResult_t e = ncclGetUniqueId(&u);
+    if (e != ncclSuccess) { SetError("ncclGetUniqueId: %s", ncclGetErrorString(e)); return (int)e; }
+    std::memcpy(id, &u, 128);
+    return 0;
+}
+
+pt_comm* ptCommCreate(pt_device* d, int nranks, int rank, const uint8_t id[128])
+{
+    if (!d || nranks < 1 || rank < 0 || rank >= nranks) { SetError("bad comm arguments"); return nullptr; }
+    if (hipSetDevice(d->id) != hipSuccess) { SetError("hipSetDevice failed"); return nullptr; }
+    ncclUniqueId u;
+    std::memcpy(&u, id, 128);
+    pt_comm* c = new pt_comm;
+    c->dev = d;
+    c->nranks = nranks;
+    c->rank = rank;
+    ncclResult_t e = ncclCommInitRank(&c->comm, nranks, u, rank);
+    if (e != ncclSuccess) { SetError("ncclCommInitRank: %s", ncclGetErrorString(e)); delete c; return nullptr; }
+    return c;
+}
+
+void ptCommDestroy(pt_comm* c)
+{
+    if (!c) return;
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    delete c;
+}
+
+int ptCommReduceSampleBuffer(pt_device* d, pt_comm* c, pt_sample_buffer* b, int root)
+{
+    if (!d || !c || !b) { SetError("null argument"); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    size_t count = (size_t)b->width * b->height * 4;
+    ncclResult_t e = ncclReduce(b->accum, b->accum, count, ncclFloat32, ncclSum, root, c->comm, d->stream);
+    if (e != ncclSuccess) { SetError("ncclReduce: %s", ncclGetErrorString(e)); return (int)e; }
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,235 @@
+"""Integrator entry points (mirror of src/integrator/basic.hpp:28-32 and
+src/integrator/integrator.hpp:51-60) over libpathtracer.so.
+
+    CreateSampleBuffer(device, W, H)          integrator.hpp:51
+    CreateBasicRenderer(device, scene, sb)     basic.hpp:28
+    ResetBasicRenderer(device, renderer)       basic.hpp:31
+    RunBasicRenderer(device, renderer, rounds) basic.hpp:32
+
+The renderer's CameraIndex / RenderFlags / PathLengthLimit /
+PathTerminationProbability / FrameIndex are exposed as attributes, written
+by the caller before Reset/Run exactly as application.cpp:104-107 does.
+Everything runs in the HIP library; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _native as N
+
+
+class PathTracerError(RuntimeError):
+    pass
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise PathTracerError(f"{what}: {N.hip_lib().ptGetLastError().decode()} (status {rc})")
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    N.hip_lib().ptGetDeviceCount(C.byref(n))
+    return n.value
+
+
+class Device:
+    """A HIP device + stream (replaces the reference's `vulkan` context)."""
+
+    def __init__(self, hip_device: int = 0):
+        L = N.hip_lib()
+        self._h = L.ptCreateDevice(int(hip_device))
+        if not self._h:
+            raise PathTracerError(L.ptGetLastError().decode())
+        self.index = hip_device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def synchronize(self):
+        _check(N.hip_lib().ptSynchronize(self._h), "ptSynchronize")
+
+    def set_profiling(self, enable: bool):
+        _check(N.hip_lib().ptSetProfiling(self._h, int(enable)), "ptSetProfiling")
+
+    def kernel_stats(self, kernel: int):
+        n = C.c_uint64(0)
+        ms = C.c_double(0)
+        _check(N.hip_lib().ptGetKernelStats(self._h, kernel, C.byref(n), C.byref(ms)), "ptGetKernelStats")
+        return int(n.value), float(ms.value)
+
+    def reset_kernel_stats(self):
+        _check(N.hip_lib().ptResetKernelStats(self._h), "ptResetKernelStats")
+
+    def close(self):
+        if self._h:
+            N.hip_lib().ptDestroyDevice(self._h)
+            self._h = None
+
+
+class DeviceScene:
+    """Device copy of a packed scene (CreateVulkanScene / UpdateVulkanScene)."""
+
+    def __init__(self, device: Device):
+        L = N.hip_lib()
+        self.device = device
+        self._h = L.ptCreateScene(device.handle)
+        if not self._h:
+            raise PathTracerError(L.ptGetLastError().decode())
+
+    @property
+    def handle(self):
+        return self._h
+
+    def update(self, scene, dirty_flags: int = 0xFFFFFFFF):
+        packs = scene.packs() if hasattr(scene, "packs") else scene
+        _check(N.hip_lib().ptUpdateScene(self.device.handle, self._h, C.byref(packs), dirty_flags), "ptUpdateScene")
+
+    def trace_rays(self, origins: np.ndarray, packed_velocities: np.ndarray, durations: np.ndarray) -> np.ndarray:
+        """Bit-exact Trace() of a ray batch (scene.glsl.inc:522-611)."""
+        o = np.ascontiguousarray(origins, dtype=np.float32).reshape(-1, 3)
+        v = np.ascontiguousarray(packed_velocities, dtype=np.uint32).reshape(-1)
+        d = np.ascontiguousarray(durations, dtype=np.float32).reshape(-1)
+        out = np.zeros(len(v), dtype=N.HIT_RECORD_DTYPE)
+        _check(N.hip_lib().ptTraceRays(self.device.handle, self._h, len(v), N.fptr(o), N.u32ptr(v), N.fptr(d),
+                                       out.ctypes.data), "ptTraceRays")
+        return out
+
+    def close(self):
+        if self._h:
+            N.hip_lib().ptDestroyScene(self.device.handle, self._h)
+            self._h = None
+
+
+class SampleBuffer:
+    """rgba32f accumulator: CIE XYZ sums + sample count (integrator.cpp:15-87)."""
+
+    def __init__(self, device: Device, width: int, height: int):
+        L = N.hip_lib()
+        self.device = device
+        self.width, self.height = int(width), int(height)
+        self._h = L.ptCreateSampleBuffer(device.handle, self.width, self.height)
+        if not self._h:
+            raise PathTracerError(L.ptGetLastError().decode())
+
+    @property
+    def handle(self):
+        return self._h
+
+    def read(self) -> np.ndarray:
+        out = np.zeros((self.height, self.width, 4), dtype=np.float32)
+        _check(N.hip_lib().ptReadSampleBuffer(self.device.handle, self._h, N.fptr(out)), "ptReadSampleBuffer")
+        return out
+
+    def close(self):
+        if self._h:
+            N.hip_lib().ptDestroySampleBuffer(self.device.handle, self._h)
+            self._h = None
+
+
+class BasicRenderer:
+    """basic_renderer (basic.hpp:6-26) running the HIP wavefront kernels."""
+
+    _FIELDS = ("FrameIndex", "CameraIndex", "RenderFlags", "PathLengthLimit", "PathTerminationProbability")
+
+    def __init__(self, device: Device, scene: DeviceScene, sample_buffer: SampleBuffer, rank: int = 0, nranks: int = 1):
+        L = N.hip_lib()
+        self.device, self.scene, self.sample_buffer = device, scene, sample_buffer
+        self.rank, self.nranks = rank, nranks
+        self._h = L.ptCreateBasicRendererPartitioned(device.handle, scene.handle, sample_buffer.handle, rank, nranks)
+        if not self._h:
+            raise PathTracerError(L.ptGetLastError().decode())
+        self._params = L.ptBasicRendererParams(self._h)
+
+    def __getattr__(self, name):
+        if name in BasicRenderer._FIELDS:
+            return getattr(self._params.contents, name)
+        raise AttributeError(name)
+
+    def __setattr__(self, name, value):
+        if name in BasicRenderer._FIELDS:
+            setattr(self._params.contents, name, value)
+        else:
+            object.__setattr__(self, name, value)
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def slot_count(self) -> int:
+        return int(N.hip_lib().ptBasicRendererSlotCount(self._h))
+
+    def reset(self):
+        _check(N.hip_lib().ptResetBasicRenderer(self.device.handle, self._h), "ptResetBasicRenderer")
+
+    def run(self, rounds: int = 1):
+        _check(N.hip_lib().ptRunBasicRenderer(self.device.handle, self._h, int(rounds)), "ptRunBasicRenderer")
+
+    def read_state(self) -> np.ndarray:
+        sb = self.sample_buffer
+        out = np.zeros(sb.width * sb.height, dtype=N.PIXEL_STATE_DTYPE)
+        _check(N.hip_lib().ptReadBasicRendererState(self.device.handle, self._h, out.ctypes.data),
+               "ptReadBasicRendererState")
+        return out.reshape(sb.height, sb.width)
+
+    def close(self):
+        if self._h:
+            N.hip_lib().ptDestroyBasicRenderer(self.device.handle, self._h)
+            self._h = None
+
+
+class Comm:
+    """RCCL communicator (one process per GPU) for the frame-end reduce."""
+
+    def __init__(self, device: Device, nranks: int, rank: int, unique_id: bytes):
+        L = N.hip_lib()
+        buf = (C.c_uint8 * 128)(*unique_id)
+        self.device = device
+        self._h = L.ptCommCreate(device.handle, nranks, rank, buf)
+        if not self._h:
+            raise PathTracerError(L.ptGetLastError().decode())
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * 128)()
+        _check(N.hip_lib().ptCommGetUniqueId(buf), "ptCommGetUniqueId")
+        return bytes(buf)
+
+    def reduce_sample_buffer(self, sample_buffer: SampleBuffer, root: int = 0):
+        _check(N.hip_lib().ptCommReduceSampleBuffer(self.device.handle, self._h, sample_buffer.handle, root),
+               "ptCommReduceSampleBuffer")
+
+    def close(self):
+        if self._h:
+            N.hip_lib().ptCommDestroy(self._h)
+            self._h = None
+
+
+# Reference-named free functions ------------------------------------------------
+
+def CreateSampleBuffer(device: Device, width: int, height: int) -> SampleBuffer:
+    return SampleBuffer(device, width, height)
+
+
+def CreateBasicRenderer(device: Device, scene: DeviceScene, sample_buffer: SampleBuffer) -> BasicRenderer:
+    return BasicRenderer(device, scene, sample_buffer)
+
+
+def ResetBasicRenderer(device: Device, renderer: BasicRenderer):
+    renderer.reset()
+
+
+def RunBasicRenderer(device: Device, renderer: BasicRenderer, rounds: int):
+    renderer.run(rounds)
+
+
+def DestroyBasicRenderer(device: Device, renderer: BasicRenderer):
+    renderer.close()
+
+
+def DestroySampleBuffer(device: Device, sample_buffer: SampleBuffer):
+    sample_buffer.close()

@@ -1,0 +1,204 @@
+"""Host scene API (mirror of the reference's src/scene/scene.hpp:410-442).
+
+Thin Python handles over libptscene.so: CreateScene / CreateEntity /
+CreateMaterial / CreateCheckerTexture / mesh creation and PackSceneData,
+keeping the reference's names and field meanings.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _native as N
+
+ENTITY_CONTAINER, ENTITY_CAMERA, ENTITY_MESH_INSTANCE, ENTITY_PLANE, ENTITY_SPHERE, ENTITY_CUBE = 1, 2, 3, 4, 5, 6
+MATERIAL_BASIC_DIFFUSE, MATERIAL_BASIC_METAL, MATERIAL_BASIC_TRANSLUCENT, MATERIAL_OPENPBR = 0, 1, 2, 3
+TEXTURE_RAW, TEXTURE_REFLECTANCE_WITH_ALPHA, TEXTURE_RADIANCE = 0, 1, 2
+SCENE_DIRTY_ALL = 0xFFFFFFFF
+RENDER_FLAG_ACCUMULATE, RENDER_FLAG_SAMPLE_JITTER = 1, 2
+
+
+def _f3(v):
+    return (C.c_float * 3)(*[float(x) for x in v]) if v is not None else None
+
+
+class Scene:
+    """A host scene (scene.hpp:335-362) and its packed buffers."""
+
+    def __init__(self, handle, info=None):
+        if not handle:
+            raise RuntimeError(N.scene_lib().ptsGetLastError().decode())
+        self._h = handle
+        self.info = info
+        self._keep = []
+
+    # -- construction --------------------------------------------------------
+    @classmethod
+    def create(cls):
+        """CreateScene (scene.cpp:912-943): checker plane + camera at (0,0,1)."""
+        return cls(N.scene_lib().ptsCreateScene())
+
+    @classmethod
+    def empty(cls):
+        return cls(N.scene_lib().ptsCreateEmptyScene())
+
+    @classmethod
+    def config(cls, config_id: int):
+        """Benchmark scene C1..C5 (BASELINE.json configs), already packed."""
+        info = N.pts_config_info()
+        h = N.scene_lib().ptsCreateConfigScene(int(config_id), C.byref(info))
+        return cls(h, info)
+
+    def close(self):
+        if self._h:
+            N.scene_lib().ptsDestroyScene(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def root(self):
+        return N.scene_lib().ptsSceneRoot(self._h)
+
+    def create_entity(self, entity_type: int, parent=None, position=None, rotation=None, scale=None, material=None):
+        L = N.scene_lib()
+        e = L.ptsCreateEntity(self._h, int(entity_type), parent)
+        if not e:
+            raise RuntimeError(L.ptsGetLastError().decode())
+        if position is not None or rotation is not None or scale is not None:
+            L.ptsSetEntityTransform(self._h, e, _f3(position), _f3(rotation), _f3(scale))
+        if material is not None:
+            L.ptsSetEntityMaterial(self._h, e, material)
+        return e
+
+    def set_transform(self, entity, position=None, rotation=None, scale=None):
+        N.scene_lib().ptsSetEntityTransform(self._h, entity, _f3(position), _f3(rotation), _f3(scale))
+
+    def set_material(self, entity, material):
+        N.scene_lib().ptsSetEntityMaterial(self._h, entity, material)
+
+    def set_mesh(self, entity, mesh):
+        N.scene_lib().ptsSetEntityMesh(self._h, entity, mesh)
+
+    def set_camera_pinhole(self, camera, fov_degrees=90.0, aperture_mm=0.0):
+        N.scene_lib().ptsSetCameraPinhole(self._h, camera, fov_degrees, aperture_mm)
+
+    def set_camera_thin_lens(self, camera, sensor_mm=(32.0, 18.0), focal_mm=20.0, aperture_mm=10.0, focus=1.0):
+        N.scene_lib().ptsSetCameraThinLens(self._h, camera, sensor_mm[0], sensor_mm[1], focal_mm, aperture_mm, focus)
+
+    def set_camera_360(self, camera):
+        N.scene_lib().ptsSetCamera360(self._h, camera)
+
+    def set_root(self, scatter_rate=0.0, skybox_brightness=1.0, skybox_sampling_probability=0.0, skybox=None):
+        N.scene_lib().ptsSetRootParameters(self._h, scatter_rate, skybox_brightness, skybox_sampling_probability, skybox)
+
+    def create_material(self, material_type: int, name: str = "Material", **params):
+        L = N.scene_lib()
+        m = L.ptsCreateMaterial(self._h, int(material_type), name.encode())
+        for k, v in params.items():
+            self.set_material_parameter(m, k, v)
+        return m
+
+    def set_material_parameter(self, material, name, value):
+        L = N.scene_lib()
+        if name.endswith("Texture"):
+            rc = L.ptsSetMaterialTexture(self._h, material, name.encode(), value)
+        else:
+            vals = np.atleast_1d(np.asarray(value, dtype=np.float32))
+            rc = L.ptsSetMaterialParameter(self._h, material, name.encode(), N.fptr(vals), len(vals))
+        if rc != 0:
+            raise ValueError(L.ptsGetLastError().decode())
+
+    def create_checker_texture(self, name, texture_type, color_a, color_b):
+        a = (C.c_float * 4)(*color_a)
+        b = (C.c_float * 4)(*color_b)
+        return N.scene_lib().ptsCreateCheckerTexture(self._h, name.encode(), int(texture_type), a, b)
+
+    def create_texture(self, name, texture_type, rgba: np.ndarray, nearest=False):
+        rgba = np.ascontiguousarray(rgba, dtype=np.float32)
+        h, w = rgba.shape[:2]
+        return N.scene_lib().ptsCreateTexture(self._h, name.encode(), int(texture_type), w, h, N.fptr(rgba), int(nearest))
+
+    def create_mesh(self, positions, indices, normals=None, uvs=None, name="Mesh"):
+        pos = np.ascontiguousarray(positions, dtype=np.float32).reshape(-1, 3)
+        idx = np.ascontiguousarray(indices, dtype=np.uint32).reshape(-1, 3)
+        nrm = None if normals is None else np.ascontiguousarray(normals, dtype=np.float32).reshape(-1, 3)
+        uv = None if uvs is None else np.ascontiguousarray(uvs, dtype=np.float32).reshape(-1, 2)
+        L = N.scene_lib()
+        m = L.ptsCreateMesh(self._h, name.encode(), len(pos), N.fptr(pos), N.fptr(nrm) if nrm is not None else None,
+                            N.fptr(uv) if uv is not None else None, len(idx), N.u32ptr(idx))
+        if not m:
+            raise ValueError(L.ptsGetLastError().decode())
+        return m
+
+    # -- packing -------------------------------------------------------------
+    def pack(self) -> int:
+        """PackSceneData (scene.cpp:1115-1621); returns the dirty flags it packed."""
+        return int(N.scene_lib().ptsPackSceneData(self._h))
+
+    def mark_dirty(self, flags=SCENE_DIRTY_ALL):
+        N.scene_lib().ptsMarkDirty(self._h, flags)
+
+    def packs(self) -> N.pt_scene_packs:
+        p = N.pt_scene_packs()
+        N.scene_lib().ptsGetScenePacks(self._h, C.byref(p))
+        return p
+
+    def arrays(self):
+        """numpy copies of every packed buffer (for tests and fixtures)."""
+        p = self.packs()
+
+        def view(ptr, count, dtype):
+            if count == 0 or not ptr:
+                return np.zeros(0, dtype=dtype)
+            buf = (C.c_char * (count * np.dtype(dtype).itemsize)).from_address(ptr)
+            return np.frombuffer(buf, dtype=dtype).copy()
+
+        return {
+            "globals": view(p.globals, 1, N.GLOBALS_DTYPE),
+            "textures": view(p.textures, p.texture_count, N.TEXTURE_DTYPE),
+            "materials": view(p.material_data, p.material_word_count, np.uint32),
+            "shapes": view(p.shapes, p.shape_count, N.SHAPE_DTYPE),
+            "shape_nodes": view(p.shape_nodes, p.shape_node_count, N.SHAPE_NODE_DTYPE),
+            "mesh_faces": view(p.mesh_faces, p.mesh_face_count, N.MESH_FACE_DTYPE),
+            "mesh_vertices": view(p.mesh_vertices, p.mesh_vertex_count, N.MESH_VERTEX_DTYPE),
+            "mesh_nodes": view(p.mesh_nodes, p.mesh_node_count, N.MESH_NODE_DTYPE),
+            "cameras": view(p.cameras, p.camera_count, N.CAMERA_DTYPE),
+        }
+
+
+def mesh_depth(mesh) -> int:
+    return int(N.scene_lib().ptsMeshDepth(mesh))
+
+
+def mesh_node_count(mesh) -> int:
+    return int(N.scene_lib().ptsMeshNodeCount(mesh))
+
+
+def spectrum_coefficients(rgb) -> np.ndarray:
+    """GetParametricSpectrumCoefficients (spectrum.cpp:439-479)."""
+    c = np.asarray(rgb, dtype=np.float32)
+    out = np.zeros(3, dtype=np.float32)
+    N.scene_lib().ptsGetParametricSpectrumCoefficients(N.fptr(c), N.fptr(out))
+    return out
+
+
+def build_spectrum_table(path: str | None = None, threads: int = 0):
+    L = N.scene_lib()
+    L.ptsBuildSpectrumTable(threads)
+    if path:
+        if L.ptsSaveSpectrumTable(str(path).encode()) != 0:
+            raise OSError(f"cannot write {path}")
+
+
+def load_spectrum_table(path) -> bool:
+    return N.scene_lib().ptsLoadSpectrumTable(str(path).encode()) == 0
