@@ -124,6 +124,11 @@ int                ptReadBasicRendererState(pt_device* device, pt_basic_renderer
 int ptTraceRays(pt_device* device, pt_scene* scene, uint32_t n, const float* origins,
                 const uint32_t* packed_velocities, const float* durations, pt_hit_record* out);
 
+/* Diagnostic: evaluates the extend kernel's exact fast division (FMA-corrected
+ * reciprocal) against IEEE division on n device-generated operand pairs and
+ * returns the number of bit mismatches (must be 0). */
+int ptCheckFastDivision(pt_device* device, uint64_t n, uint32_t seed, uint64_t* mismatches);
+
 /* Per-kernel device time, measured with HIP events on the renderer stream. */
 int ptSetProfiling(pt_device* device, int enable);
 int ptGetKernelStats(pt_device* device, int kernel, uint64_t* launches, double* total_ms);

@@ -20,111 +20,73 @@ namespace ptd {
 
 // --- traversal stack: LDS columns + global spill ----------------------------
 
-template <bool SPILL>
+template <bool SPILL, int CAP>
 struct tstack {
     uint32_t* lds;        // &smem[tid]; entry i at lds[i * 256]
-    uint32_t* spill;      // &spill[slot]; entry i (>= PT_LDS_STACK) at spill[(i - CAP) * stride]
+    uint32_t* spill;      // &spill[thread]; entry i (>= CAP) at spill[(i - CAP) * stride]
     uint32_t stride;
     PT_DEV void put(uint32_t i, uint32_t v)
     {
-        if (!SPILL || i < PT_LDS_STACK) lds[i * 256] = v;
-        else spill[(i - PT_LDS_STACK) * stride] = v;
+        if (!SPILL || i < CAP) lds[i * 256] = v;
+        else spill[(i - CAP) * stride] = v;
     }
     PT_DEV uint32_t get(uint32_t i) const
     {
-        if (!SPILL || i < PT_LDS_STACK) return lds[i * 256];
-        return spill[(i - PT_LDS_STACK) * stride];
+        if (!SPILL || i < CAP) return lds[i * 256];
+        return spill[(i - CAP) * stride];
     }
 };
 
-struct thit {
-    float Time;
-    uint32_t ShapeIndex;
-    uint32_t ShapeType;
-    uint32_t PrimitiveIndex;
-    pt3 Coords;
+// --- persistent traversal ---------------------------------------------------
+//
+// Trace() (scene.glsl.inc:468-611) as a resumable state machine: every loop
+// iteration advances each active lane by ONE node of its own traversal, in
+// exactly the reference's order (near-first children, LIFO Stack[32] per
+// level, IntersectShape at TLAS leaves, IntersectMeshNode for mesh instances),
+// so every ray reaches the same closest hit bit for bit.  Lanes whose ray is
+// finished take the next ray of the wave's chunk, so the 64 lanes of a wave
+// stay busy instead of idling behind the longest ray (Aila & Laine style
+// persistent threads with dynamic fetch).
+
+struct lane_state {
+    pt3 O, V, Y;         // current-level ray (world at TLAS level, object space
+                         // inside a mesh) and its reciprocal velocity
+    float Time;          // Hit.Time
+    uint32_t Shape;      // Hit.ShapeIndex (0xFFFFFFFE = face of the current mesh)
+    uint32_t Prim;       // Hit.PrimitiveIndex
+    pt3 C;               // Hit.PrimitiveCoordinates
+    uint32_t na, nb;     // node being processed: TLAS {ChildNodeIndices, ShapeIndex},
+                         // BLAS {FaceBeginOrNodeIndex, FaceEndIndex}
+    uint32_t dT, dB;     // TLAS / BLAS stack depths (<= 32 each)
+    uint32_t blas;       // shape index of the mesh being traversed, NONE at TLAS level
 };
 
-// IntersectMeshFace (scene.glsl.inc:304-334)
-PT_DEV void IntersectMeshFace(const dscene& S, pt3 O, pt3 V, uint32_t F, thit& H)
+PT_DEV void LaneBegin(const dscene& S, lane_state& L, pt3 O, pt3 V, float Duration)
 {
-    float4 a = S.mesh_faces[3 * F + 0], b = S.mesh_faces[3 * F + 1], c = S.mesh_faces[3 * F + 2];
-    pt3 P0 = xyz(a), P1 = xyz(b), P2 = xyz(c);
-    pt3 Edge1 = P1 - P0;
-    pt3 Edge2 = P2 - P0;
-    pt3 RCE2 = cross(V, Edge2);
-    float Det = dot(Edge1, RCE2);
-    if (pt_abs(Det) < PT_EPSILON) return;
-    float InvDet = 1.0f / Det;
-    pt3 Sv = O - P0;
-    float U = InvDet * dot(Sv, RCE2);
-    if (U < 0 || U > 1) return;
-    pt3 SCE1 = cross(Sv, Edge1);
-    float W = InvDet * dot(V, SCE1);
-    if (W < 0 || U + W > 1) return;
-    float T = InvDet * dot(Edge2, SCE1);
-    if (T < 0 || T > H.Time) return;
-    H.Time = T;
-    H.ShapeType = PT_SHAPE_TYPE_MESH_INSTANCE;
-    H.ShapeIndex = 0xFFFFFFFEu;
-    H.PrimitiveIndex = F;
-    H.Coords = v3(1 - U - W, U, W);
+    L.O = O;
+    L.V = V;
+    L.Y = RecipForDiv3(V);
+    L.Time = Duration;
+    L.Shape = SHAPE_INDEX_NONE;
+    L.Prim = 0;
+    L.C = v3s(0);
+    L.dT = 0;
+    L.dB = 0;
+    L.blas = SHAPE_INDEX_NONE;
+    L.na = __float_as_uint(S.shape_nodes[0].w);
+    L.nb = __float_as_uint(S.shape_nodes[1].w);
 }
 
-// IntersectMeshNode (scene.glsl.inc:336-399); BLAS entries are stacked above
-// the TLAS entries (base), 32 per level like the reference's Stack[32].
-template <bool SPILL>
-PT_DEV void IntersectMeshNode(const dscene& S, pt3 O, pt3 V, uint32_t Root, thit& H, tstack<SPILL>& st, uint32_t base)
+// IntersectShape for the analytic shapes (scene.glsl.inc:413-465).
+PT_DEV void IntersectAnalytic(int32_t Type, pt3 O, pt3 V, uint32_t ShapeIndex, lane_state& L)
 {
-    uint32_t Depth = 0;
-    float4 n0 = S.mesh_nodes[2 * Root], n1 = S.mesh_nodes[2 * Root + 1];
-    while (true) {
-        uint32_t Begin = __float_as_uint(n0.w), End = __float_as_uint(n1.w);
-        if (End > 0) {
-            for (uint32_t F = Begin; F < End; F++) IntersectMeshFace(S, O, V, F, H);
-        } else {
-            uint32_t Index = Begin;
-            n0 = S.mesh_nodes[2 * Index]; n1 = S.mesh_nodes[2 * Index + 1];
-            float TimeA = IntersectBoundingBox(O, V, H.Time, n0, n1);
-            float4 m0 = S.mesh_nodes[2 * Index + 2], m1 = S.mesh_nodes[2 * Index + 3];
-            float TimeB = IntersectBoundingBox(O, V, H.Time, m0, m1);
-            if (TimeA > TimeB) {
-                if (TimeA < PT_INFINITY && Depth < 32) st.put(base + Depth++, Index);
-                n0 = m0; n1 = m1;
-                continue;
-            }
-            if (TimeB < PT_INFINITY) {
-                if (Depth < 32) st.put(base + Depth++, Index + 1);
-                continue;
-            }
-            if (TimeA < PT_INFINITY) continue;
-        }
-        if (Depth == 0) break;
-        uint32_t I = st.get(base + --Depth);
-        n0 = S.mesh_nodes[2 * I]; n1 = S.mesh_nodes[2 * I + 1];
-    }
-}
-
-// IntersectShape (scene.glsl.inc:401-466)
-template <bool SPILL>
-PT_DEV void IntersectShape(const dscene& S, pt3 WO, pt3 WV, uint32_t ShapeIndex, thit& H, tstack<SPILL>& st, uint32_t base)
-{
-    const pt_packed_shape* Shape = &S.shapes[ShapeIndex];
-    const float* From = Shape->Transform.From;
-    pt3 O = mat4_mul_point(From, WO);
-    pt3 V = mat4_mul_vector(From, WV);
-    int32_t Type = Shape->Type;
-    if (Type == PT_SHAPE_TYPE_MESH_INSTANCE) {
-        IntersectMeshNode<SPILL>(S, O, V, Shape->MeshRootNodeIndex, H, st, base);
-        if (H.ShapeIndex == 0xFFFFFFFEu) H.ShapeIndex = ShapeIndex;
-    } else if (Type == PT_SHAPE_TYPE_PLANE) {
+    if (Type == PT_SHAPE_TYPE_PLANE) {
         float T = -O.z / V.z;
-        if (T < 0 || T > H.Time) return;
-        H.Time = T;
-        H.ShapeType = PT_SHAPE_TYPE_PLANE;
-        H.ShapeIndex = ShapeIndex;
-        H.PrimitiveIndex = 0;
-        H.Coords = O + V * T;
+        if (T < 0 || T > L.Time) return;
+        L.Time = T;
+        L.Shape = ShapeIndex;
+        L.Prim = 0;
+        L.C = O + V * T;
     } else if (Type == PT_SHAPE_TYPE_SPHERE) {
         float Vv = dot(V, V);
         float P = dot(O, V);
@@ -136,88 +98,164 @@ PT_DEV void IntersectShape(const dscene& S, pt3 WO, pt3 WV, uint32_t ShapeIndex,
         float S0 = -P - D;
         float S1 = -P + D;
         float Sv = S0 < 0 ? S1 : S0;
-        if (Sv < 0 || Sv > Vv * H.Time) return;
-        H.Time = Sv / Vv;
-        H.ShapeType = PT_SHAPE_TYPE_SPHERE;
-        H.ShapeIndex = ShapeIndex;
-        H.PrimitiveIndex = 0;
-        H.Coords = O + V * H.Time;
+        if (Sv < 0 || Sv > Vv * L.Time) return;
+        L.Time = Sv / Vv;
+        L.Shape = ShapeIndex;
+        L.Prim = 0;
+        L.C = O + V * L.Time;
     } else if (Type == PT_SHAPE_TYPE_CUBE) {
         pt3 Mn = (v3s(-1) - O) / V;
         pt3 Mx = (v3s(+1) - O) / V;
         pt3 E = vmin(Mn, Mx);
-        pt3 L = vmax(Mn, Mx);
+        pt3 Lt = vmax(Mn, Mx);
         float T0 = pt_max(pt_max(E.x, E.y), E.z);
-        float T1 = pt_min(pt_min(L.x, L.y), L.z);
+        float T1 = pt_min(pt_min(Lt.x, Lt.y), Lt.z);
         if (T1 < T0) return;
         if (T1 <= 0) return;
         float T = T0 < 0 ? T1 : T0;
-        if (T >= H.Time) return;
-        H.Time = T;
-        H.ShapeType = PT_SHAPE_TYPE_CUBE;
-        H.ShapeIndex = ShapeIndex;
-        H.PrimitiveIndex = 0;
-        H.Coords = O + V * T;
+        if (T >= L.Time) return;
+        L.Time = T;
+        L.Shape = ShapeIndex;
+        L.Prim = 0;
+        L.C = O + V * T;
     }
 }
 
-// Trace (scene.glsl.inc:468-611) -> packed hit record.
-template <bool SPILL>
-PT_DEV void TraceRecord(const dscene& S, pt3 O, pt3 V, float Duration, tstack<SPILL>& st, float4& rec, float2& uv,
-                        bool& isHit)
+// IntersectMeshFace (scene.glsl.inc:304-334) on the lane's object-space ray.
+PT_DEV void LaneMeshFace(const dscene& S, uint32_t F, lane_state& L)
 {
-    thit H;
-    H.ShapeIndex = SHAPE_INDEX_NONE;
-    H.Time = Duration;
-    H.ShapeType = 0;
-    H.PrimitiveIndex = 0;
-    H.Coords = v3s(0);
-    if (S.g.ShapeCount != 0) {
-        uint32_t Depth = 0;
-        float4 a0 = S.shape_nodes[0], a1 = S.shape_nodes[1];
-        while (true) {
-            uint32_t Children = __float_as_uint(a0.w);
-            if (Children == 0) {
-                IntersectShape<SPILL>(S, O, V, __float_as_uint(a1.w), H, st, Depth);
-            } else {
-                uint32_t IA = Children & 0xFFFF, IB = Children >> 16;
-                a0 = S.shape_nodes[2 * IA]; a1 = S.shape_nodes[2 * IA + 1];
-                float4 b0 = S.shape_nodes[2 * IB], b1 = S.shape_nodes[2 * IB + 1];
-                float TA = IntersectBoundingBox(O, V, H.Time, a0, a1);
-                float TB = IntersectBoundingBox(O, V, H.Time, b0, b1);
-                if (TA > TB) {
-                    if (TA < PT_INFINITY && Depth < 32) st.put(Depth++, IA);
-                    a0 = b0; a1 = b1;
-                    continue;
-                }
-                if (TB < PT_INFINITY) {
-                    if (Depth < 32) st.put(Depth++, IB);
-                    continue;
-                }
-                if (TA < PT_INFINITY) continue;
+    float4 a = S.mesh_faces[3 * F + 0], b = S.mesh_faces[3 * F + 1], c = S.mesh_faces[3 * F + 2];
+    pt3 P0 = xyz(a);
+    pt3 Edge1 = xyz(b) - P0;
+    pt3 Edge2 = xyz(c) - P0;
+    pt3 RCE2 = cross(L.V, Edge2);
+    float Det = dot(Edge1, RCE2);
+    if (pt_abs(Det) < PT_EPSILON) return;
+    float InvDet = 1.0f / Det;
+    pt3 Sv = L.O - P0;
+    float U = InvDet * dot(Sv, RCE2);
+    if (U < 0 || U > 1) return;
+    pt3 SCE1 = cross(Sv, Edge1);
+    float W = InvDet * dot(L.V, SCE1);
+    if (W < 0 || U + W > 1) return;
+    float T = InvDet * dot(Edge2, SCE1);
+    if (T < 0 || T > L.Time) return;
+    L.Time = T;
+    L.Shape = 0xFFFFFFFEu;
+    L.Prim = F;
+    L.C = v3(1 - U - W, U, W);
+}
+
+// Advances one lane by one node.  Returns true when its Trace() is complete.
+// Only the two index words of the current node are carried between steps;
+// its bounds were already consumed by the parent's box test.
+template <bool SPILL, int CAP, class Src>
+PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, const Src& src, uint32_t slot)
+{
+    const uint32_t* mesh_words = reinterpret_cast<const uint32_t*>(S.mesh_nodes);
+    const uint32_t* shape_words = reinterpret_cast<const uint32_t*>(S.shape_nodes);
+    if (L.blas != SHAPE_INDEX_NONE) {
+        // IntersectMeshNode (scene.glsl.inc:336-399), one node.
+        if (L.nb > 0) {
+            for (uint32_t F = L.na; F < L.nb; F++) LaneMeshFace(S, F, L);
+        } else {
+            uint32_t Index = L.na;
+            float4 a0 = S.mesh_nodes[2 * Index], a1 = S.mesh_nodes[2 * Index + 1];
+            float4 b0 = S.mesh_nodes[2 * Index + 2], b1 = S.mesh_nodes[2 * Index + 3];
+            float TA = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, a0, a1);
+            float TB = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, b0, b1);
+            if (TA > TB) {
+                if (TA < PT_INFINITY && L.dB < 32) st.put(L.dT + L.dB++, Index);
+                L.na = __float_as_uint(b0.w); L.nb = __float_as_uint(b1.w);
+                return false;
             }
-            if (Depth == 0) break;
-            uint32_t I = st.get(--Depth);
-            a0 = S.shape_nodes[2 * I]; a1 = S.shape_nodes[2 * I + 1];
+            if (TB < PT_INFINITY) {
+                if (L.dB < 32) st.put(L.dT + L.dB++, Index + 1);
+                L.na = __float_as_uint(a0.w); L.nb = __float_as_uint(a1.w);
+                return false;
+            }
+            if (TA < PT_INFINITY) { L.na = __float_as_uint(a0.w); L.nb = __float_as_uint(a1.w); return false; }
+        }
+        if (L.dB > 0) {
+            uint32_t I = st.get(L.dT + --L.dB);
+            L.na = mesh_words[8 * I + 3];
+            L.nb = mesh_words[8 * I + 7];
+            return false;
+        }
+        // IntersectMeshNode returned (scene.glsl.inc:409-411); back to the
+        // world-space ray for the rest of the shape traversal.
+        if (L.Shape == 0xFFFFFFFEu) L.Shape = L.blas;
+        L.blas = SHAPE_INDEX_NONE;
+        if (L.dT == 0) return true;
+        float D;
+        src.load(slot, L.O, L.V, D);
+        L.Y = RecipForDiv3(L.V);
+    } else {
+        // Intersect (scene.glsl.inc:468-520), one node.
+        uint32_t Children = L.na;
+        if (Children == 0) {
+            uint32_t ShapeIndex = L.nb;
+            const pt_packed_shape* Shape = &S.shapes[ShapeIndex];
+            const float* From = Shape->Transform.From;
+            pt3 O = mat4_mul_point(From, L.O);
+            pt3 V = mat4_mul_vector(From, L.V);
+            int32_t Type = Shape->Type;
+            if (Type == PT_SHAPE_TYPE_MESH_INSTANCE) {
+                uint32_t Root = Shape->MeshRootNodeIndex;
+                L.O = O;
+                L.V = V;
+                L.Y = RecipForDiv3(V);
+                L.blas = ShapeIndex;
+                L.dB = 0;
+                L.na = mesh_words[8 * Root + 3];
+                L.nb = mesh_words[8 * Root + 7];
+                return false;
+            }
+            IntersectAnalytic(Type, O, V, ShapeIndex, L);
+        } else {
+            uint32_t IA = Children & 0xFFFF, IB = Children >> 16;
+            float4 a0 = S.shape_nodes[2 * IA], a1 = S.shape_nodes[2 * IA + 1];
+            float4 b0 = S.shape_nodes[2 * IB], b1 = S.shape_nodes[2 * IB + 1];
+            float TA = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, a0, a1);
+            float TB = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, b0, b1);
+            if (TA > TB) {
+                if (TA < PT_INFINITY && L.dT < 32) st.put(L.dT++, IA);
+                L.na = __float_as_uint(b0.w); L.nb = __float_as_uint(b1.w);
+                return false;
+            }
+            if (TB < PT_INFINITY) {
+                if (L.dT < 32) st.put(L.dT++, IB);
+                L.na = __float_as_uint(a0.w); L.nb = __float_as_uint(a1.w);
+                return false;
+            }
+            if (TA < PT_INFINITY) { L.na = __float_as_uint(a0.w); L.nb = __float_as_uint(a1.w); return false; }
         }
     }
-    isHit = H.ShapeIndex != SHAPE_INDEX_NONE;
-    if (!isHit) return;
+    if (L.dT > 0) {
+        uint32_t I = st.get(--L.dT);
+        L.na = shape_words[8 * I + 3];
+        L.nb = shape_words[8 * I + 7];
+        return false;
+    }
+    return true;
+}
 
-    const pt_packed_shape* Shape = &S.shapes[H.ShapeIndex];
-    uint32_t MaterialIndex = Shape->MaterialIndex;
+// Hit attribute reconstruction (scene.glsl.inc:535-608).
+PT_DEV void HitAttributes(const dscene& S, uint32_t ShapeIndex, uint32_t Prim, pt3 C, uint32_t& Material, pt3& Normal,
+                          pt3& TangentX, pt2& UV)
+{
+    const pt_packed_shape* Shape = &S.shapes[ShapeIndex];
+    Material = Shape->MaterialIndex;
+    int32_t Type = Shape->Type;
     const float* To = Shape->Transform.To;
     const float* From = Shape->Transform.From;
-    pt3 Normal, TangentX;
-    pt2 UV;
-    if (H.ShapeType == PT_SHAPE_TYPE_MESH_INSTANCE) {
-        float4 f0 = S.mesh_faces[3 * H.PrimitiveIndex + 0];
-        float4 f1 = S.mesh_faces[3 * H.PrimitiveIndex + 1];
-        float4 f2 = S.mesh_faces[3 * H.PrimitiveIndex + 2];
+    if (Type == PT_SHAPE_TYPE_MESH_INSTANCE) {
+        float4 f0 = S.mesh_faces[3 * Prim + 0];
+        float4 f1 = S.mesh_faces[3 * Prim + 1];
+        float4 f2 = S.mesh_faces[3 * Prim + 2];
         uint2 V0 = S.mesh_vertices[__float_as_uint(f0.w)];
         uint2 V1 = S.mesh_vertices[__float_as_uint(f1.w)];
         uint2 V2 = S.mesh_vertices[__float_as_uint(f2.w)];
-        pt3 C = H.Coords;
         pt3 N = SafeNormalize(UnpackUnitVector(V0.x) * C.x + UnpackUnitVector(V1.x) * C.y + UnpackUnitVector(V2.x) * C.z);
         Normal = TransformNormal(N, From);
         TangentX = ComputeTangentVector(Normal);
@@ -225,19 +263,19 @@ PT_DEV void TraceRecord(const dscene& S, pt3 O, pt3 V, float Duration, tstack<SP
         pt2 UV1 = v2(pt_half_to_float(V1.y & 0xFFFF), pt_half_to_float(V1.y >> 16));
         pt2 UV2 = v2(pt_half_to_float(V2.y & 0xFFFF), pt_half_to_float(V2.y >> 16));
         UV = UV0 * C.x + UV1 * C.y + UV2 * C.z;
-    } else if (H.ShapeType == PT_SHAPE_TYPE_PLANE) {
+    } else if (Type == PT_SHAPE_TYPE_PLANE) {
         Normal = TransformNormal(v3(0, 0, 1), From);
         TangentX = TransformDirection(v3(1, 0, 0), To);
-        UV = v2(pt_fract(H.Coords.x), pt_fract(H.Coords.y));
-    } else if (H.ShapeType == PT_SHAPE_TYPE_SPHERE) {
-        pt3 P = H.Coords;
+        UV = v2(pt_fract(C.x), pt_fract(C.y));
+    } else if (Type == PT_SHAPE_TYPE_SPHERE) {
+        pt3 P = C;
         float U = (pt_atan2(P.y, P.x) + PT_PI) / PT_TAU;
         float W = (P.z + 1.0f) / 2.0f;
         Normal = TransformNormal(P, From);
         TangentX = TransformDirection(cross(P, v3(-P.y, P.x, 0)), To);
         UV = v2(U, W);
     } else {
-        pt3 P = H.Coords;
+        pt3 P = C;
         pt3 Q = vabs(P);
         pt3 N, T;
         if (Q.x >= Q.y && Q.x >= Q.z) {
@@ -256,12 +294,6 @@ PT_DEV void TraceRecord(const dscene& S, pt3 O, pt3 V, float Duration, tstack<SP
         Normal = TransformNormal(N, From);
         TangentX = TransformDirection(T, To);
     }
-    // StoreTraceHit (basic.glsl.inc:142-157)
-    rec.x = H.Time;
-    rec.y = __uint_as_float((H.ShapeIndex << 16) | MaterialIndex);
-    rec.z = __uint_as_float(PackUnitVector(Normal));
-    rec.w = __uint_as_float(PackUnitVector(TangentX));
-    uv = make_float2(UV.x, UV.y);
 }
 
 // --- slot / pixel mapping ---------------------------------------------------
@@ -695,31 +727,169 @@ __global__ __launch_bounds__(256) void raygen_kernel(dscene S, dslots L, dframe 
     F.accum[(size_t)y * F.width + x] = make_float4(0, 0, 0, 0);
 }
 
-template <bool SPILL>
-__global__ __launch_bounds__(256) void extend_kernel(dscene S, dslots L, dframe F)
-{
-    __shared__ uint32_t smem[PT_LDS_STACK * 256];
-    uint32_t s = blockIdx.x * 256 + threadIdx.x;
-    if (s >= L.n) return;
-    uint32_t x, y;
-    if (!SlotPixel(F, s, x, y)) return;
-    float4 r = L.ray[s];
-    pt3 O = v3(r.x, r.y, r.z);
-    pt3 V = UnpackUnitVector(__float_as_uint(r.w));
-    tstack<SPILL> st;
-    st.lds = &smem[threadIdx.x];
-    st.spill = L.spill + s;
-    st.stride = L.n;
-    float4 rec;
-    float2 uv;
-    bool isHit;
-    TraceRecord<SPILL>(S, O, V, PT_HIT_TIME_LIMIT, st, rec, uv, isHit);
-    if (isHit) {
-        L.hit[s] = rec;
-        L.uv[s] = uv;
-    } else {
-        reinterpret_cast<uint32_t*>(&L.hit[s])[1] = 0xFFFFFFFFu;
+// Persistent extend: blocks of 256 threads, one chunk cursor per wave.  The
+// slot range is split into 8 segments with one dequeue counter each (blocks
+// start on segment blockIdx % 8, i.e. on "their" XCD under round-robin
+// placement — speed only), and a wave moves on to the next segment once its
+// own is drained.  counters[0..7] are zeroed by the launcher before every
+// launch; every wave exits once all 8 are drained and its lanes are idle.
+struct ray_source_slots {
+    dslots L;
+    dframe F;
+    PT_DEV bool load(uint32_t s, pt3& O, pt3& V, float& D) const
+    {
+        uint32_t x, y;
+        if (!SlotPixel(F, s, x, y)) return false;
+        float4 r = L.ray[s];
+        O = v3(r.x, r.y, r.z);
+        V = UnpackUnitVector(__float_as_uint(r.w));
+        D = PT_HIT_TIME_LIMIT;
+        return true;
     }
+    PT_DEV void store(uint32_t s, const lane_state& Ln) const
+    {
+        L.hit[s] = make_float4(Ln.Time, __uint_as_float(Ln.Shape), __uint_as_float(Ln.Prim), Ln.C.x);
+        L.uv[s] = make_float2(Ln.C.y, Ln.C.z);
+    }
+};
+
+struct ray_source_arrays {
+    const float* origins;
+    const uint32_t* vel;
+    const float* dur;
+    float4* hit;
+    float2* hc;
+    PT_DEV bool load(uint32_t i, pt3& O, pt3& V, float& D) const
+    {
+        O = v3(origins[3 * i], origins[3 * i + 1], origins[3 * i + 2]);
+        V = UnpackUnitVector(vel[i]);
+        D = dur[i];
+        return true;
+    }
+    PT_DEV void store(uint32_t i, const lane_state& Ln) const
+    {
+        hit[i] = make_float4(Ln.Time, __uint_as_float(Ln.Shape), __uint_as_float(Ln.Prim), Ln.C.x);
+        hc[i] = make_float2(Ln.C.y, Ln.C.z);
+    }
+};
+
+constexpr uint32_t PT_CHUNK = 128;
+constexpr uint32_t PT_SEGMENTS = 8;
+
+template <class Src, bool SPILL, int MINW, int CAP>
+__global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, uint32_t n, uint32_t* counters,
+                                                           uint32_t* spill, uint32_t spill_stride)
+{
+    __shared__ uint32_t smem[CAP * 256];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t seg = ((n + PT_SEGMENTS - 1) / PT_SEGMENTS + PT_CHUNK - 1) / PT_CHUNK * PT_CHUNK;
+    tstack<SPILL, CAP> st;
+    st.lds = &smem[threadIdx.x];
+    st.spill = spill + (blockIdx.x * 256 + threadIdx.x);
+    st.stride = spill_stride;
+
+    uint32_t cur = 0, end = 0;                    // wave-uniform chunk cursor
+    uint32_t segi = blockIdx.x % PT_SEGMENTS, tries = 0;
+    bool drained = false;
+    bool active = false;
+    uint32_t slot = 0;
+    lane_state Ln;
+
+    while (true) {
+        if (!drained) {
+            uint64_t idle = __ballot(!active);
+            while (idle != 0) {
+                if (cur >= end) {
+                    bool got = false;
+                    while (tries < PT_SEGMENTS) {
+                        uint32_t sb = segi * seg;
+                        uint32_t se = min(sb + seg, n);
+                        uint32_t off = 0;
+                        if (lane == 0) off = atomicAdd(&counters[segi], PT_CHUNK);
+                        off = __builtin_amdgcn_readfirstlane(off);
+                        if (sb < se && off < se - sb) {
+                            cur = sb + off;
+                            end = min(cur + PT_CHUNK, se);
+                            got = true;
+                            break;
+                        }
+                        segi = (segi + 1) % PT_SEGMENTS;
+                        tries++;
+                    }
+                    if (!got) { drained = true; break; }
+                }
+                uint32_t avail = end - cur;
+                uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                if (!active && rank < avail) {
+                    slot = cur + rank;
+                    pt3 O, V;
+                    float D;
+                    if (src.load(slot, O, V, D)) {
+                        LaneBegin(S, Ln, O, V, D);
+                        if (S.g.ShapeCount != 0) active = true;
+                        else src.store(slot, Ln);
+                    }
+                }
+                cur += min((uint32_t)__popcll(idle), avail);
+                idle = __ballot(!active);
+            }
+        }
+        if (__ballot(active) == 0) break;
+        if (active) {
+            if (LaneStep<SPILL, CAP>(S, Ln, st, src, slot)) {
+                src.store(slot, Ln);
+                active = false;
+            }
+        }
+    }
+}
+
+// One ray per thread (no dynamic fetch): the same LaneStep state machine run
+// to completion by each thread for its own slot.
+template <class Src, bool SPILL, int MINW, int CAP>
+__global__ __launch_bounds__(256, MINW) void extend_simple_kernel(dscene S, Src src, uint32_t n, uint32_t* spill,
+                                                                  uint32_t spill_stride)
+{
+    __shared__ uint32_t smem[CAP * 256];
+    uint32_t slot = blockIdx.x * 256 + threadIdx.x;
+    if (slot >= n) return;
+    tstack<SPILL, CAP> st;
+    st.lds = &smem[threadIdx.x];
+    st.spill = spill + slot;
+    st.stride = spill_stride;
+    pt3 O, V;
+    float D;
+    if (!src.load(slot, O, V, D)) return;
+    lane_state Ln;
+    LaneBegin(S, Ln, O, V, D);
+    if (S.g.ShapeCount != 0)
+        while (!LaneStep<SPILL, CAP>(S, Ln, st, src, slot)) {}
+    src.store(slot, Ln);
+}
+
+// Compact hit -> the reference's packed trace record (StoreTraceHit,
+// basic.glsl.inc:142-157): {time, shape<<16|material, packed normal, packed
+// tangent} + uv.  Used by the ray-query API and the state readback.
+__global__ __launch_bounds__(256) void finalize_kernel(dscene S, uint32_t n, const float4* hit, const float2* hc,
+                                                       float4* rec, float2* uv)
+{
+    uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float4 h = hit[i];
+    uint32_t Shape = __float_as_uint(h.y);
+    if (Shape == SHAPE_INDEX_NONE) {
+        rec[i] = make_float4(0, __uint_as_float(0xFFFFFFFFu), 0, 0);
+        uv[i] = make_float2(0, 0);
+        return;
+    }
+    float2 c = hc[i];
+    uint32_t Material;
+    pt3 N, TX;
+    pt2 UV;
+    HitAttributes(S, Shape, __float_as_uint(h.z), v3(h.w, c.x, c.y), Material, N, TX, UV);
+    rec[i] = make_float4(h.x, __uint_as_float((Shape << 16) | Material), __uint_as_float(PackUnitVector(N)),
+                         __uint_as_float(PackUnitVector(TX)));
+    uv[i] = make_float2(UV.x, UV.y);
 }
 
 __global__ __launch_bounds__(256) void shade_kernel(dscene S, dslots L, dframe F, dparams Pm)
@@ -744,24 +914,27 @@ __global__ __launch_bounds__(256) void shade_kernel(dscene S, dslots L, dframe F
     for (int I = 0; I < 4; I++)
         if (P.Active[I] == 0xFFFF) P.Active[I] = SHAPE_INDEX_NONE;
 
-    // LoadTraceResult (basic.glsl.inc:99-131)
+    // LoadTraceResult (basic.glsl.inc:99-131).  The extend kernel leaves a
+    // compact hit; the trace record's attributes (Trace, scene.glsl.inc:
+    // 535-608) are rebuilt here and go through the same octahedral snorm16
+    // quantisation as the reference's StoreTraceHit / LoadTraceResult.
     float4 r = L.ray[s];
     pt3 O = v3(r.x, r.y, r.z);
     pt3 V = UnpackUnitVector(__float_as_uint(r.w));
     float4 h = L.hit[s];
-    uint32_t sm = __float_as_uint(h.y);
-    uint32_t HitShape = SHAPE_INDEX_NONE, HitMaterial = 0;
+    uint32_t HitShape = __float_as_uint(h.y), HitMaterial = 0;
     float HitTime = PT_HIT_TIME_LIMIT;
     uint32_t PN = 0, PTg = 0;
     pt2 UV = v2(0, 0);
-    if (sm != 0xFFFFFFFFu) {
-        HitShape = sm >> 16;
-        HitMaterial = sm & 0xFFFF;
+    if (HitShape != SHAPE_INDEX_NONE) {
+        float2 c = L.uv[s];
+        pt3 N, TX;
+        HitAttributes(S, HitShape, __float_as_uint(h.z), v3(h.w, c.x, c.y), HitMaterial, N, TX, UV);
+        HitMaterial &= 0xFFFFu;
+        HitShape &= 0xFFFFu;
         HitTime = h.x;
-        PN = __float_as_uint(h.z);
-        PTg = __float_as_uint(h.w);
-        float2 uv = L.uv[s];
-        UV = v2(uv.x, uv.y);
+        PN = PackUnitVector(N);
+        PTg = PackUnitVector(TX);
     }
 
     if (Scatter(S, G, Pm.termination_probability, P, O, V, HitShape, HitMaterial, HitTime, PN, PTg, UV)) {
@@ -779,30 +952,27 @@ __global__ __launch_bounds__(256) void shade_kernel(dscene S, dslots L, dframe F
     }
 }
 
-template <bool SPILL>
-__global__ __launch_bounds__(256) void trace_rays_kernel(dscene S, uint32_t n, const float* origins,
-                                                         const uint32_t* vel, const float* dur, float4* out_rec,
-                                                         float2* out_uv, uint32_t* spill)
+// Checks XDiv against IEEE division on device-generated operands: counts
+// mismatching bit patterns (test infrastructure for the convention).
+__global__ __launch_bounds__(256) void xdiv_check_kernel(uint64_t n, uint32_t seed, unsigned long long* mismatches)
 {
-    __shared__ uint32_t smem[PT_LDS_STACK * 256];
-    uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    pt3 O = v3(origins[3 * i], origins[3 * i + 1], origins[3 * i + 2]);
-    pt3 V = UnpackUnitVector(vel[i]);
-    tstack<SPILL> st;
-    st.lds = &smem[threadIdx.x];
-    st.spill = spill + i;
-    st.stride = n;
-    float4 rec;
-    float2 uv;
-    bool isHit;
-    TraceRecord<SPILL>(S, O, V, dur[i], st, rec, uv, isHit);
-    if (!isHit) {
-        rec = make_float4(0, __uint_as_float(0xFFFFFFFFu), 0, 0);
-        uv = make_float2(0, 0);
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint64_t stride = (uint64_t)gridDim.x * 256;
+    unsigned long long bad = 0;
+    for (; i < n; i += stride) {
+        uint32_t s = (uint32_t)i * 2654435761u ^ seed;
+        uint32_t ra = pt_random(&s), rb = pt_random(&s), rc = pt_random(&s);
+        // exponents spread over +-2^40 around 1, random signs and mantissas
+        float a = pt_u2f(((87u + (ra >> 26) + (rc & 15)) << 23) | (ra & 0x7fffffu) | ((rc >> 31) << 31));
+        float b = pt_u2f(((107u + ((rb >> 27) & 31)) << 23) | (rb & 0x7fffffu) | (((rc >> 30) & 1u) << 31));
+        if ((rc & 0xff0) == 0) a = 0.0f;
+        if ((rc & 0xff00) == 0) b = 0.0f;
+        float y = RecipForDiv(b);
+        float q = XDiv(a, b, y);
+        float e = a / b;
+        if (pt_f2u(q) != pt_f2u(e) && !(q != q && e != e)) bad++;
     }
-    out_rec[i] = rec;
-    out_uv[i] = uv;
+    if (bad) atomicAdd(mismatches, bad);
 }
 
 }  // namespace ptd
@@ -821,13 +991,79 @@ hipError_t pt_launch_raygen(const ptd::dscene& S, const ptd::dslots& L, const pt
     return hipGetLastError();
 }
 
-hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, bool spill,
-                            hipStream_t st)
+// Occupancy variants of the extend kernel: {min waves per SIMD, LDS stack
+// entries}.  Selected by pt_extend_variant() (PT_EXTEND_VARIANT, default 0).
+#define PT_EXTEND_VARIANTS(X) X(0, 4, 24) X(1, 6, 16) X(3, 5, 20)
+#define PT_EXTEND_SIMPLE_VARIANTS(X) X(5, 4, 24) X(6, 5, 20)
+
+int pt_extend_variant()
+{
+    static int v = []() {
+        const char* e = getenv("PT_EXTEND_VARIANT");
+        int x = e ? atoi(e) : 0;
+        return (x == 0 || x == 1 || x == 3 || x == 5 || x == 6) ? x : 0;
+    }();
+    return v;
+}
+
+uint32_t pt_extend_stack_cap()
+{
+    switch (pt_extend_variant()) {
+#define X(id, w, cap) case id: return cap;
+        PT_EXTEND_VARIANTS(X)
+        PT_EXTEND_SIMPLE_VARIANTS(X)
+#undef X
+    }
+    return 24;
+}
+
+template <class Src>
+static hipError_t LaunchExtendVariant(const ptd::dscene& S, const Src& src, uint32_t n, uint32_t* counters,
+                                      uint32_t* spill, uint32_t grid_blocks, hipStream_t st)
+{
+    uint32_t stride = grid_blocks * 256;
+    switch (pt_extend_variant()) {
+#define X(id, w, cap)                                                                                               \
+    case id:                                                                                                       \
+        if (spill)                                                                                                 \
+            hipLaunchKernelGGL((ptd::extend_kernel<Src, true, w, cap>), dim3(grid_blocks), dim3(256), 0, st, S, src, \
+                               n, counters, spill, stride);                                                        \
+        else                                                                                                       \
+            hipLaunchKernelGGL((ptd::extend_kernel<Src, false, w, cap>), dim3(grid_blocks), dim3(256), 0, st, S,   \
+                               src, n, counters, spill, stride);                                                   \
+        break;
+        PT_EXTEND_VARIANTS(X)
+#undef X
+#define X(id, w, cap)                                                                                               \
+    case id:                                                                                                       \
+        if (spill)                                                                                                 \
+            hipLaunchKernelGGL((ptd::extend_simple_kernel<Src, true, w, cap>), dim3(Blocks(n)), dim3(256), 0, st, S, \
+                               src, n, spill, n);                                                                  \
+        else                                                                                                       \
+            hipLaunchKernelGGL((ptd::extend_simple_kernel<Src, false, w, cap>), dim3(Blocks(n)), dim3(256), 0, st,   \
+                               S, src, n, spill, n);                                                               \
+        break;
+        PT_EXTEND_SIMPLE_VARIANTS(X)
+#undef X
+    }
+    return hipGetLastError();
+}
+
+// Spill rows are per persistent thread for the queue variants, per ray for
+// the one-ray-per-thread variants.
+uint32_t pt_extend_spill_threads(uint32_t grid_blocks, uint32_t n)
+{
+    return pt_extend_variant() >= 5 ? n : grid_blocks * 256;
+}
+
+hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* counters,
+                            uint32_t* spill, uint32_t grid_blocks, hipStream_t st)
 {
     if (L.n == 0) return hipSuccess;
-    if (spill) hipLaunchKernelGGL(ptd::extend_kernel<true>, dim3(Blocks(L.n)), dim3(256), 0, st, S, L, F);
-    else hipLaunchKernelGGL(ptd::extend_kernel<false>, dim3(Blocks(L.n)), dim3(256), 0, st, S, L, F);
-    return hipGetLastError();
+    hipError_t e = hipMemsetAsync(counters, 0, 32, st);
+    if (e != hipSuccess) return e;
+    ptd::ray_source_slots src{L, F};
+    return LaunchExtendVariant(S, src, L.n, counters, spill, grid_blocks, st);
 }
 
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
@@ -838,11 +1074,47 @@ hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd
     return hipGetLastError();
 }
 
+hipError_t pt_launch_xdiv_check(uint64_t n, uint32_t seed, unsigned long long* mismatches, hipStream_t st)
+{
+    hipLaunchKernelGGL(ptd::xdiv_check_kernel, dim3(4096), dim3(256), 0, st, n, seed, mismatches);
+    return hipGetLastError();
+}
+
 hipError_t pt_launch_trace_rays(const ptd::dscene& S, uint32_t n, const float* origins, const uint32_t* vel,
-                                const float* dur, float4* rec, float2* uv, uint32_t* spill, hipStream_t st)
+                                const float* dur, float4* hit, float2* hc, float4* rec, float2* uv, uint32_t* counters,
+                                uint32_t* spill, uint32_t grid_blocks, hipStream_t st)
 {
     if (n == 0) return hipSuccess;
-    if (spill) hipLaunchKernelGGL(ptd::trace_rays_kernel<true>, dim3(Blocks(n)), dim3(256), 0, st, S, n, origins, vel, dur, rec, uv, spill);
-    else hipLaunchKernelGGL(ptd::trace_rays_kernel<false>, dim3(Blocks(n)), dim3(256), 0, st, S, n, origins, vel, dur, rec, uv, spill);
+    hipError_t e = hipMemsetAsync(counters, 0, 32, st);
+    if (e != hipSuccess) return e;
+    ptd::ray_source_arrays src{origins, vel, dur, hit, hc};
+    if ((e = LaunchExtendVariant(S, src, n, counters, spill, grid_blocks, st)) != hipSuccess) return e;
+    return pt_launch_finalize(S, n, hit, hc, rec, uv, st);
+}
+
+hipError_t pt_launch_finalize(const ptd::dscene& S, uint32_t n, const float4* hit, const float2* hc, float4* rec,
+                              float2* uv, hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(ptd::finalize_kernel, dim3(Blocks(n)), dim3(256), 0, st, S, n, hit, hc, rec, uv);
     return hipGetLastError();
+}
+
+uint32_t pt_extend_blocks_per_cu(bool spill)
+{
+    int blocks = 0;
+    hipError_t e = hipErrorUnknown;
+    switch (pt_extend_variant()) {
+#define X(id, w, cap)                                                                                             \
+    case id:                                                                                                     \
+        e = spill ? hipOccupancyMaxActiveBlocksPerMultiprocessor(                                                \
+                        &blocks, ptd::extend_kernel<ptd::ray_source_slots, true, w, cap>, 256, 0)                \
+                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(                                                \
+                        &blocks, ptd::extend_kernel<ptd::ray_source_slots, false, w, cap>, 256, 0);              \
+        break;
+        PT_EXTEND_VARIANTS(X)
+#undef X
+    }
+    if (e != hipSuccess || blocks < 1) blocks = 1;
+    return (uint32_t)blocks;
 }

@@ -9,7 +9,7 @@
 // deeper entries go to a per-slot global spill area (only allocated when the
 // scene's BVH depths need it).
 #ifndef PT_LDS_STACK
-#define PT_LDS_STACK 16
+#define PT_LDS_STACK 24
 #endif
 
 namespace ptd {
@@ -19,13 +19,13 @@ struct dscene;
 // Per-slot state, SoA of 16-byte records.
 struct dslots {
     float4* ray;        // origin.xyz, packed velocity
-    float4* hit;        // time, shape<<16|material, packed normal, packed tangent
-    float2* uv;
+    float4* hit;        // compact hit: time, shape index, primitive index, coords.x
+    float2* uv;         // compact hit: coords.y, coords.z
     float4* thr;        // throughput[4]
     float4* prob;       // probability[4]
     float4* smp;        // sample.xyz, normalized lambda0
     uint2* act;         // active-shape stack (2 x u16 pairs)
-    uint32_t* spill;    // traversal stack spill, (64 - PT_LDS_STACK) x n
+    uint32_t* spill;    // traversal stack spill, rows x (persistent threads)
     uint32_t n;
 };
 
@@ -47,9 +47,17 @@ struct dparams {
 
 hipError_t pt_launch_raygen(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
                             hipStream_t st);
-hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, bool spill,
-                            hipStream_t st);
+hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* counters,
+                            uint32_t* spill, uint32_t grid_blocks, hipStream_t st);
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
                            hipStream_t st);
+hipError_t pt_launch_xdiv_check(uint64_t n, uint32_t seed, unsigned long long* mismatches, hipStream_t st);
 hipError_t pt_launch_trace_rays(const ptd::dscene& S, uint32_t n, const float* origins, const uint32_t* vel,
-                                const float* dur, float4* rec, float2* uv, uint32_t* spill, hipStream_t st);
+                                const float* dur, float4* hit, float2* hc, float4* rec, float2* uv, uint32_t* counters,
+                                uint32_t* spill, uint32_t grid_blocks, hipStream_t st);
+hipError_t pt_launch_finalize(const ptd::dscene& S, uint32_t n, const float4* hit, const float2* hc, float4* rec,
+                              float2* uv, hipStream_t st);
+uint32_t pt_extend_blocks_per_cu(bool spill);
+int pt_extend_variant();
+uint32_t pt_extend_stack_cap();
+uint32_t pt_extend_spill_threads(uint32_t grid_blocks, uint32_t n);

@@ -91,11 +91,46 @@ PT_DEV pt3 UnpackUnitVector(uint32_t P)
     return normalize(v3(Px, Py, Z));
 }
 
-// Slab test (common.glsl.inc:153-185) with true division.
-PT_DEV float IntersectBoundingBox(pt3 O, pt3 V, float Reach, float4 MinAndX, float4 MaxAndX)
+// Correctly rounded a / b given y = RN(1/b) (precomputed once per ray):
+// q = RN(a*y), one FMA residual correction (Markstein) -> RN(a/b).  Outside
+// the guarded range (b or a/b beyond 2^+-100, b = 0, a = 0, NaN) it falls
+// back to IEEE division, so the result is always bit-identical to a / b
+// (the convention of include/pt_fp.h); tests/test_gpu_parity.py checks this
+// over >10^9 operand pairs on the device.
+PT_DEV float RecipForDiv(float b)
 {
-    pt3 MinT = (xyz(MinAndX) - O) / V;
-    pt3 MaxT = (xyz(MaxAndX) - O) / V;
+    float m = pt_abs(b);
+    return (m >= 0x1p-100f && m <= 0x1p100f) ? 1.0f / b : pt_u2f(0x7fc00000u);
+}
+
+PT_DEV float XDiv(float a, float b, float y)
+{
+    float q = a * y;
+    float r = __builtin_fmaf(-q, b, a);
+    float q1 = __builtin_fmaf(r, y, q);
+    float m = pt_abs(q1);
+    if (!(m >= 0x1p-100f && m <= 0x1p100f)) q1 = a / b;
+    return q1;
+}
+
+// Fast quotient without the range guard; `bad` accumulates whether the guard
+// would have fired (q1 outside [2^-100, 2^100] and a != 0, or NaN).  A zero
+// numerator may give a zero of the other sign than IEEE a / b; the slab test
+// only compares its quotients, so the sign of a zero is unobservable there.
+PT_DEV float XDivNoGuard(float a, float b, float y, bool& bad)
+{
+    float q = a * y;
+    float r = __builtin_fmaf(-q, b, a);
+    float q1 = __builtin_fmaf(r, y, q);
+    float m = pt_abs(q1);
+    bad |= !(m <= 0x1p100f) | ((m < 0x1p-100f) & (a != 0.0f));
+    return q1;
+}
+
+PT_DEV pt3 RecipForDiv3(pt3 b) { return v3(RecipForDiv(b.x), RecipForDiv(b.y), RecipForDiv(b.z)); }
+
+PT_DEV float SlabEntry(pt3 MinT, pt3 MaxT, float Reach)
+{
     float Ex = pt_min(MinT.x, MaxT.x), Ey = pt_min(MinT.y, MaxT.y), Ez = pt_min(MinT.z, MaxT.z);
     float Lx = pt_max(MinT.x, MaxT.x), Ly = pt_max(MinT.y, MaxT.y), Lz = pt_max(MinT.z, MaxT.z);
     float EntryT = pt_max(pt_max(Ex, Ey), Ez);
@@ -104,6 +139,23 @@ PT_DEV float IntersectBoundingBox(pt3 O, pt3 V, float Reach, float4 MinAndX, flo
     if (ExitT <= 0) return PT_INFINITY;
     if (EntryT >= Reach) return PT_INFINITY;
     return EntryT;
+}
+
+// Slab test (common.glsl.inc:153-185).  The six divisions by the ray velocity
+// use the exact fast quotient; if any of them leaves the range where that is
+// proven (rare: zero velocity components, extreme scales) the whole box is
+// recomputed with IEEE division.
+PT_DEV float IntersectBoundingBox(pt3 O, pt3 V, pt3 Y, float Reach, float4 MinAndX, float4 MaxAndX)
+{
+    pt3 A = xyz(MinAndX) - O, B = xyz(MaxAndX) - O;
+    bool bad = false;
+    pt3 MinT = v3(XDivNoGuard(A.x, V.x, Y.x, bad), XDivNoGuard(A.y, V.y, Y.y, bad), XDivNoGuard(A.z, V.z, Y.z, bad));
+    pt3 MaxT = v3(XDivNoGuard(B.x, V.x, Y.x, bad), XDivNoGuard(B.y, V.y, Y.y, bad), XDivNoGuard(B.z, V.z, Y.z, bad));
+    if (bad) {
+        MinT = A / V;
+        MaxT = B / V;
+    }
+    return SlabEntry(MinT, MaxT, Reach);
 }
 
 struct rng {

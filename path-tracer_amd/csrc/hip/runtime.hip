@@ -76,6 +76,8 @@ struct event_pair { hipEvent_t a, b; int kernel; };
 struct pt_device {
     int id = 0;
     hipStream_t stream = nullptr;
+    uint32_t cu_count = 256;
+    uint32_t* counters = nullptr;     // 8 dequeue counters of the persistent extend kernel
     bool profiling = false;
     std::vector<event_pair> pending;
     std::vector<event_pair> free_events;
@@ -242,6 +244,7 @@ int ValidatePacks(const pt_scene_packs* p, uint32_t* stack_needed)
         if (g.ShapeCount != p->shape_count) { SetError("packs: ShapeCount %u != shape_count %u", g.ShapeCount, p->shape_count); return -1; }
         if (p->shape_node_count == 0) { SetError("packs: no shape nodes"); return -1; }
     }
+    if (p->shape_count > 65535 || p->shape_node_count > 65536) { SetError("packs: more than 65535 shapes (16-bit indices)"); return -1; }
     if (!TexOk(g.SkyboxTextureIndex, p->texture_count)) { SetError("packs: bad skybox texture"); return -1; }
     if (p->texture_count > 0 && (!p->atlas || p->atlas_layer_count == 0 || p->atlas_width == 0 || p->atlas_height == 0)) {
         SetError("packs: textures without atlas"); return -1;
@@ -293,12 +296,17 @@ ptd::dparams Params(pt_basic_renderer* r, uint32_t seed)
     return P;
 }
 
-int EnsureSpill(pt_basic_renderer* r)
+uint32_t ExtendGrid(pt_device* d, bool spill)
 {
-    uint32_t need = r->scene->stack_needed;
-    if (need <= PT_LDS_STACK) { r->slots.spill = nullptr; return 0; }
-    size_t rows = need - PT_LDS_STACK;
-    PT_HIP(r->spill.alloc(rows * (size_t)r->slots.n));
+    return d->cu_count * pt_extend_blocks_per_cu(spill);
+}
+
+int EnsureSpill(pt_basic_renderer* r, uint32_t grid)
+{
+    uint32_t need = r->scene->stack_needed, cap = pt_extend_stack_cap();
+    if (need <= cap) { r->slots.spill = nullptr; return 0; }
+    size_t rows = need - cap;
+    PT_HIP(r->spill.alloc(rows * (size_t)pt_extend_spill_threads(grid, r->slots.n)));
     r->slots.spill = r->spill.ptr;
     return 0;
 }
@@ -337,8 +345,13 @@ pt_device* ptCreateDevice(int hip_device)
     if (hipSetDevice(hip_device) != hipSuccess) { SetError("hipSetDevice(%d) failed", hip_device); return nullptr; }
     pt_device* d = new pt_device;
     d->id = hip_device;
-    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
-        SetError("hipStreamCreate failed");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess && prop.multiProcessorCount > 0)
+        d->cu_count = (uint32_t)prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&d->counters, 64) != hipSuccess) {
+        SetError("device stream / counter allocation failed");
+        if (d->stream) (void)hipStreamDestroy(d->stream);
         delete d;
         return nullptr;
     }
@@ -352,6 +365,7 @@ void ptDestroyDevice(pt_device* d)
     (void)hipStreamSynchronize(d->stream);
     for (auto& ep : d->pending) { (void)hipEventDestroy(ep.a); (void)hipEventDestroy(ep.b); }
     for (auto& ep : d->free_events) { (void)hipEventDestroy(ep.a); (void)hipEventDestroy(ep.b); }
+    if (d->counters) (void)hipFree(d->counters);
     (void)hipStreamDestroy(d->stream);
     delete d;
 }
@@ -542,15 +556,16 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
     if (!d) { SetError("null device"); return -1; }
     if (CheckReady(r) != 0) return -1;
     PT_HIP(hipSetDevice(d->id));
-    if (int e = EnsureSpill(r)) return e;
+    bool spill = r->scene->stack_needed > pt_extend_stack_cap();
+    uint32_t grid = ExtendGrid(d, spill);
+    if (int e = EnsureSpill(r, grid)) return e;
     r->params.FrameIndex += 1;
     ptd::dparams P = Params(r, r->params.FrameIndex);
     ptd::dframe F = Frame(r);
-    bool spill = r->slots.spill != nullptr;
     for (uint32_t i = 0; i < rounds; i++) {
         event_pair ep{};
         if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep)) return e;
-        PT_HIP(pt_launch_extend(r->scene->d, r->slots, F, spill, d->stream));
+        PT_HIP(pt_launch_extend(r->scene->d, r->slots, F, d->counters, r->slots.spill, grid, d->stream));
         if (int e = EndTimed(d, ep)) return e;
         if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep)) return e;
         PT_HIP(pt_launch_shade(r->scene->d, r->slots, F, P, d->stream));
@@ -568,12 +583,25 @@ int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state*
     std::vector<float4> ray(n), hit(n), thr(n), prob(n), smp(n);
     std::vector<float2> uv(n);
     std::vector<uint2> act(n);
+    if (n && r->scene->valid) {
+        // The slots hold compact hits; rebuild the reference's packed trace
+        // records (normal, tangent, uv, material) for the readback.
+        dbuf<float4> rec;
+        dbuf<float2> ruv;
+        PT_HIP(rec.alloc(n));
+        PT_HIP(ruv.alloc(n));
+        hipError_t e = pt_launch_finalize(r->scene->d, n, r->hit.ptr, r->uv.ptr, rec.ptr, ruv.ptr, d->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
+        if (e == hipSuccess) e = hipMemcpy(hit.data(), rec.ptr, (size_t)n * 16, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(uv.data(), ruv.ptr, (size_t)n * 8, hipMemcpyDeviceToHost);
+        rec.release();
+        ruv.release();
+        PT_HIP(e);
+    }
     PT_HIP(hipMemcpy(ray.data(), r->ray.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
-    PT_HIP(hipMemcpy(hit.data(), r->hit.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
     PT_HIP(hipMemcpy(thr.data(), r->thr.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
     PT_HIP(hipMemcpy(prob.data(), r->prob.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
     PT_HIP(hipMemcpy(smp.data(), r->smp.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
-    PT_HIP(hipMemcpy(uv.data(), r->uv.ptr, (size_t)n * 8, hipMemcpyDeviceToHost));
     PT_HIP(hipMemcpy(act.data(), r->act.ptr, (size_t)n * 8, hipMemcpyDeviceToHost));
     uint32_t W = r->buffer->width, H = r->buffer->height;
     auto bits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
@@ -607,37 +635,28 @@ int ptTraceRays(pt_device* d, pt_scene* s, uint32_t n, const float* origins, con
     if (!s->valid) { SetError("scene has no valid packs"); return -1; }
     if (n == 0) return 0;
     PT_HIP(hipSetDevice(d->id));
-    float *d_o = nullptr, *d_t = nullptr;
-    uint32_t *d_v = nullptr, *d_spill = nullptr;
-    float4* d_rec = nullptr;
-    float2* d_uv = nullptr;
-    int rc = 0;
-    auto cleanup = [&]() {
-        if (d_o) (void)hipFree(d_o);
-        if (d_t) (void)hipFree(d_t);
-        if (d_v) (void)hipFree(d_v);
-        if (d_spill) (void)hipFree(d_spill);
-        if (d_rec) (void)hipFree(d_rec);
-        if (d_uv) (void)hipFree(d_uv);
-    };
+    bool spill = s->stack_needed > pt_extend_stack_cap();
+    uint32_t grid = ExtendGrid(d, spill);
+    dbuf<float> d_o, d_t;
+    dbuf<uint32_t> d_v, d_spill;
+    dbuf<float4> d_hit, d_rec;
+    dbuf<float2> d_hc, d_uv;
+    hipError_t e = hipSuccess;
     do {
-        hipError_t e;
-        if ((e = hipMalloc(&d_o, (size_t)n * 12)) != hipSuccess) { rc = e; break; }
-        if ((e = hipMalloc(&d_t, (size_t)n * 4)) != hipSuccess) { rc = e; break; }
-        if ((e = hipMalloc(&d_v, (size_t)n * 4)) != hipSuccess) { rc = e; break; }
-        if ((e = hipMalloc(&d_rec, (size_t)n * 16)) != hipSuccess) { rc = e; break; }
-        if ((e = hipMalloc(&d_uv, (size_t)n * 8)) != hipSuccess) { rc = e; break; }
-        if (s->stack_needed > PT_LDS_STACK)
-            if ((e = hipMalloc(&d_spill, (size_t)(s->stack_needed - PT_LDS_STACK) * n * 4)) != hipSuccess) { rc = e; break; }
-        if ((e = hipMemcpy(d_o, origins, (size_t)n * 12, hipMemcpyHostToDevice)) != hipSuccess) { rc = e; break; }
-        if ((e = hipMemcpy(d_t, dur, (size_t)n * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = e; break; }
-        if ((e = hipMemcpy(d_v, vel, (size_t)n * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = e; break; }
-        if ((e = pt_launch_trace_rays(s->d, n, d_o, d_v, d_t, d_rec, d_uv, d_spill, d->stream)) != hipSuccess) { rc = e; break; }
-        if ((e = hipStreamSynchronize(d->stream)) != hipSuccess) { rc = e; break; }
+        if ((e = d_o.upload(origins, (size_t)n * 3)) != hipSuccess) break;
+        if ((e = d_t.upload(dur, n)) != hipSuccess) break;
+        if ((e = d_v.upload(vel, n)) != hipSuccess) break;
+        if ((e = d_hit.alloc(n)) != hipSuccess || (e = d_rec.alloc(n)) != hipSuccess) break;
+        if ((e = d_hc.alloc(n)) != hipSuccess || (e = d_uv.alloc(n)) != hipSuccess) break;
+        if (spill && (e = d_spill.alloc((size_t)(s->stack_needed - pt_extend_stack_cap()) * pt_extend_spill_threads(grid, n))) != hipSuccess) break;
+        e = pt_launch_trace_rays(s->d, n, d_o.ptr, d_v.ptr, d_t.ptr, d_hit.ptr, d_hc.ptr, d_rec.ptr, d_uv.ptr,
+                                 d->counters, spill ? d_spill.ptr : nullptr, grid, d->stream);
+        if (e != hipSuccess) break;
+        if ((e = hipStreamSynchronize(d->stream)) != hipSuccess) break;
         std::vector<float4> rec(n);
         std::vector<float2> uv(n);
-        if ((e = hipMemcpy(rec.data(), d_rec, (size_t)n * 16, hipMemcpyDeviceToHost)) != hipSuccess) { rc = e; break; }
-        if ((e = hipMemcpy(uv.data(), d_uv, (size_t)n * 8, hipMemcpyDeviceToHost)) != hipSuccess) { rc = e; break; }
+        if ((e = hipMemcpy(rec.data(), d_rec.ptr, (size_t)n * 16, hipMemcpyDeviceToHost)) != hipSuccess) break;
+        if ((e = hipMemcpy(uv.data(), d_uv.ptr, (size_t)n * 8, hipMemcpyDeviceToHost)) != hipSuccess) break;
         for (uint32_t i = 0; i < n; i++) {
             std::memcpy(&out[i].time, &rec[i].x, 4);
             std::memcpy(&out[i].shape_material, &rec[i].y, 4);
@@ -647,9 +666,27 @@ int ptTraceRays(pt_device* d, pt_scene* s, uint32_t n, const float* origins, con
             out[i].v = uv[i].y;
         }
     } while (0);
-    if (rc) SetError("ptTraceRays: %s", hipGetErrorString((hipError_t)rc));
-    cleanup();
-    return rc;
+    d_o.release(); d_t.release(); d_v.release(); d_spill.release();
+    d_hit.release(); d_rec.release(); d_hc.release(); d_uv.release();
+    if (e != hipSuccess) { SetError("ptTraceRays: %s", hipGetErrorString(e)); return (int)e; }
+    return 0;
+}
+
+int ptCheckFastDivision(pt_device* d, uint64_t n, uint32_t seed, uint64_t* mismatches)
+{
+    if (!d || !mismatches) { SetError("null argument"); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    unsigned long long* dm = nullptr;
+    PT_HIP(hipMalloc(&dm, sizeof(unsigned long long)));
+    hipError_t e = hipMemsetAsync(dm, 0, sizeof(unsigned long long), d->stream);
+    if (e == hipSuccess) e = pt_launch_xdiv_check(n, seed, dm, d->stream);
+    unsigned long long h = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, dm, sizeof(h), hipMemcpyDeviceToHost, d->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
+    (void)hipFree(dm);
+    if (e != hipSuccess) { SetError("ptCheckFastDivision: %s", hipGetErrorString(e)); return (int)e; }
+    *mismatches = h;
+    return 0;
 }
 
 int ptSetProfiling(pt_device* d, int enable)

@@ -64,6 +64,11 @@ class Device:
     def reset_kernel_stats(self):
         _check(N.hip_lib().ptResetKernelStats(self._h), "ptResetKernelStats")
 
+    def check_fast_division(self, n: int, seed: int = 1) -> int:
+        m = C.c_uint64(0)
+        _check(N.hip_lib().ptCheckFastDivision(self._h, n, seed, C.byref(m)), "ptCheckFastDivision")
+        return int(m.value)
+
     def close(self):
         if self._h:
             N.hip_lib().ptDestroyDevice(self._h)
