@@ -37,16 +37,14 @@ struct tstack {
     }
 };
 
-// --- persistent traversal ---------------------------------------------------
+// --- traversal ------------------------------------------------------------------
 //
 // Trace() (scene.glsl.inc:468-611) as a resumable state machine: every loop
 // iteration advances each active lane by ONE node of its own traversal, in
 // exactly the reference's order (near-first children, LIFO Stack[32] per
 // level, IntersectShape at TLAS leaves, IntersectMeshNode for mesh instances),
-// so every ray reaches the same closest hit bit for bit.  Lanes whose ray is
-// finished take the next ray of the wave's chunk, so the 64 lanes of a wave
-// stay busy instead of idling behind the longest ray (Aila & Laine style
-// persistent threads with dynamic fetch).
+// so every ray reaches the same closest hit bit for bit.  One flat loop over
+// both levels keeps a single loop-carried state (no nested divergent loops).
 
 struct lane_state {
     pt3 O, V, Y;         // current-level ray (world at TLAS level, object space
@@ -727,12 +725,8 @@ __global__ __launch_bounds__(256) void raygen_kernel(dscene S, dslots L, dframe 
     F.accum[(size_t)y * F.width + x] = make_float4(0, 0, 0, 0);
 }
 
-// Persistent extend: blocks of 256 threads, one chunk cursor per wave.  The
-// slot range is split into 8 segments with one dequeue counter each (blocks
-// start on segment blockIdx % 8, i.e. on "their" XCD under round-robin
-// placement — speed only), and a wave moves on to the next segment once its
-// own is drained.  counters[0..7] are zeroed by the launcher before every
-// launch; every wave exits once all 8 are drained and its lanes are idle.
+// Ray sources of the extend kernel: the renderer's slots, or the arrays of
+// the ray-query API.
 struct ray_source_slots {
     dslots L;
     dframe F;
@@ -773,81 +767,11 @@ struct ray_source_arrays {
     }
 };
 
-constexpr uint32_t PT_CHUNK = 128;
-constexpr uint32_t PT_SEGMENTS = 8;
-
+// Extend: one ray per thread, LaneStep run to completion.  (A persistent
+// variant with per-wave dynamic ray fetch was measured 1.6x slower on C3: the
+// refill bookkeeping cost more than the idle lanes it recovered.)
 template <class Src, bool SPILL, int MINW, int CAP>
-__global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, uint32_t n, uint32_t* counters,
-                                                           uint32_t* spill, uint32_t spill_stride)
-{
-    __shared__ uint32_t smem[CAP * 256];
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t seg = ((n + PT_SEGMENTS - 1) / PT_SEGMENTS + PT_CHUNK - 1) / PT_CHUNK * PT_CHUNK;
-    tstack<SPILL, CAP> st;
-    st.lds = &smem[threadIdx.x];
-    st.spill = spill + (blockIdx.x * 256 + threadIdx.x);
-    st.stride = spill_stride;
-
-    uint32_t cur = 0, end = 0;                    // wave-uniform chunk cursor
-    uint32_t segi = blockIdx.x % PT_SEGMENTS, tries = 0;
-    bool drained = false;
-    bool active = false;
-    uint32_t slot = 0;
-    lane_state Ln;
-
-    while (true) {
-        if (!drained) {
-            uint64_t idle = __ballot(!active);
-            while (idle != 0) {
-                if (cur >= end) {
-                    bool got = false;
-                    while (tries < PT_SEGMENTS) {
-                        uint32_t sb = segi * seg;
-                        uint32_t se = min(sb + seg, n);
-                        uint32_t off = 0;
-                        if (lane == 0) off = atomicAdd(&counters[segi], PT_CHUNK);
-                        off = __builtin_amdgcn_readfirstlane(off);
-                        if (sb < se && off < se - sb) {
-                            cur = sb + off;
-                            end = min(cur + PT_CHUNK, se);
-                            got = true;
-                            break;
-                        }
-                        segi = (segi + 1) % PT_SEGMENTS;
-                        tries++;
-                    }
-                    if (!got) { drained = true; break; }
-                }
-                uint32_t avail = end - cur;
-                uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-                if (!active && rank < avail) {
-                    slot = cur + rank;
-                    pt3 O, V;
-                    float D;
-                    if (src.load(slot, O, V, D)) {
-                        LaneBegin(S, Ln, O, V, D);
-                        if (S.g.ShapeCount != 0) active = true;
-                        else src.store(slot, Ln);
-                    }
-                }
-                cur += min((uint32_t)__popcll(idle), avail);
-                idle = __ballot(!active);
-            }
-        }
-        if (__ballot(active) == 0) break;
-        if (active) {
-            if (LaneStep<SPILL, CAP>(S, Ln, st, src, slot)) {
-                src.store(slot, Ln);
-                active = false;
-            }
-        }
-    }
-}
-
-// One ray per thread (no dynamic fetch): the same LaneStep state machine run
-// to completion by each thread for its own slot.
-template <class Src, bool SPILL, int MINW, int CAP>
-__global__ __launch_bounds__(256, MINW) void extend_simple_kernel(dscene S, Src src, uint32_t n, uint32_t* spill,
+__global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, uint32_t n, uint32_t* spill,
                                                                   uint32_t spill_stride)
 {
     __shared__ uint32_t smem[CAP * 256];
@@ -992,16 +916,16 @@ hipError_t pt_launch_raygen(const ptd::dscene& S, const ptd::dslots& L, const pt
 }
 
 // Occupancy variants of the extend kernel: {min waves per SIMD, LDS stack
-// entries}.  Selected by pt_extend_variant() (PT_EXTEND_VARIANT, default 0).
-#define PT_EXTEND_VARIANTS(X) X(0, 4, 24) X(1, 6, 16) X(3, 5, 20)
-#define PT_EXTEND_SIMPLE_VARIANTS(X) X(5, 4, 24) X(6, 5, 20)
+// entries per thread}.  Selected with PT_EXTEND_VARIANT (default 0); stack
+// entries beyond the LDS capacity spill to a global buffer.
+#define PT_EXTEND_VARIANTS(X) X(0, 5, 20) X(1, 4, 24) X(2, 6, 16) X(3, 4, 32)
 
 int pt_extend_variant()
 {
     static int v = []() {
         const char* e = getenv("PT_EXTEND_VARIANT");
         int x = e ? atoi(e) : 0;
-        return (x == 0 || x == 1 || x == 3 || x == 5 || x == 6) ? x : 0;
+        return (x >= 0 && x <= 3) ? x : 0;
     }();
     return v;
 }
@@ -1011,59 +935,35 @@ uint32_t pt_extend_stack_cap()
     switch (pt_extend_variant()) {
 #define X(id, w, cap) case id: return cap;
         PT_EXTEND_VARIANTS(X)
-        PT_EXTEND_SIMPLE_VARIANTS(X)
 #undef X
     }
-    return 24;
+    return 20;
 }
 
 template <class Src>
-static hipError_t LaunchExtendVariant(const ptd::dscene& S, const Src& src, uint32_t n, uint32_t* counters,
-                                      uint32_t* spill, uint32_t grid_blocks, hipStream_t st)
+static hipError_t LaunchExtend(const ptd::dscene& S, const Src& src, uint32_t n, uint32_t* spill, hipStream_t st)
 {
-    uint32_t stride = grid_blocks * 256;
+    if (n == 0) return hipSuccess;
     switch (pt_extend_variant()) {
-#define X(id, w, cap)                                                                                               \
-    case id:                                                                                                       \
-        if (spill)                                                                                                 \
-            hipLaunchKernelGGL((ptd::extend_kernel<Src, true, w, cap>), dim3(grid_blocks), dim3(256), 0, st, S, src, \
-                               n, counters, spill, stride);                                                        \
-        else                                                                                                       \
-            hipLaunchKernelGGL((ptd::extend_kernel<Src, false, w, cap>), dim3(grid_blocks), dim3(256), 0, st, S,   \
-                               src, n, counters, spill, stride);                                                   \
+#define X(id, w, cap)                                                                                           \
+    case id:                                                                                                   \
+        if (spill)                                                                                             \
+            hipLaunchKernelGGL((ptd::extend_kernel<Src, true, w, cap>), dim3(Blocks(n)), dim3(256), 0, st, S,    \
+                               src, n, spill, n);                                                              \
+        else                                                                                                   \
+            hipLaunchKernelGGL((ptd::extend_kernel<Src, false, w, cap>), dim3(Blocks(n)), dim3(256), 0, st, S,   \
+                               src, n, spill, n);                                                              \
         break;
         PT_EXTEND_VARIANTS(X)
-#undef X
-#define X(id, w, cap)                                                                                               \
-    case id:                                                                                                       \
-        if (spill)                                                                                                 \
-            hipLaunchKernelGGL((ptd::extend_simple_kernel<Src, true, w, cap>), dim3(Blocks(n)), dim3(256), 0, st, S, \
-                               src, n, spill, n);                                                                  \
-        else                                                                                                       \
-            hipLaunchKernelGGL((ptd::extend_simple_kernel<Src, false, w, cap>), dim3(Blocks(n)), dim3(256), 0, st,   \
-                               S, src, n, spill, n);                                                               \
-        break;
-        PT_EXTEND_SIMPLE_VARIANTS(X)
 #undef X
     }
     return hipGetLastError();
 }
 
-// Spill rows are per persistent thread for the queue variants, per ray for
-// the one-ray-per-thread variants.
-uint32_t pt_extend_spill_threads(uint32_t grid_blocks, uint32_t n)
+hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* spill,
+                            hipStream_t st)
 {
-    return pt_extend_variant() >= 5 ? n : grid_blocks * 256;
-}
-
-hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* counters,
-                            uint32_t* spill, uint32_t grid_blocks, hipStream_t st)
-{
-    if (L.n == 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(counters, 0, 32, st);
-    if (e != hipSuccess) return e;
-    ptd::ray_source_slots src{L, F};
-    return LaunchExtendVariant(S, src, L.n, counters, spill, grid_blocks, st);
+    return LaunchExtend(S, ptd::ray_source_slots{L, F}, L.n, spill, st);
 }
 
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
@@ -1081,14 +981,11 @@ hipError_t pt_launch_xdiv_check(uint64_t n, uint32_t seed, unsigned long long* m
 }
 
 hipError_t pt_launch_trace_rays(const ptd::dscene& S, uint32_t n, const float* origins, const uint32_t* vel,
-                                const float* dur, float4* hit, float2* hc, float4* rec, float2* uv, uint32_t* counters,
-                                uint32_t* spill, uint32_t grid_blocks, hipStream_t st)
+                                const float* dur, float4* hit, float2* hc, float4* rec, float2* uv, uint32_t* spill,
+                                hipStream_t st)
 {
-    if (n == 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(counters, 0, 32, st);
+    hipError_t e = LaunchExtend(S, ptd::ray_source_arrays{origins, vel, dur, hit, hc}, n, spill, st);
     if (e != hipSuccess) return e;
-    ptd::ray_source_arrays src{origins, vel, dur, hit, hc};
-    if ((e = LaunchExtendVariant(S, src, n, counters, spill, grid_blocks, st)) != hipSuccess) return e;
     return pt_launch_finalize(S, n, hit, hc, rec, uv, st);
 }
 
@@ -1098,23 +995,4 @@ hipError_t pt_launch_finalize(const ptd::dscene& S, uint32_t n, const float4* hi
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(ptd::finalize_kernel, dim3(Blocks(n)), dim3(256), 0, st, S, n, hit, hc, rec, uv);
     return hipGetLastError();
-}
-
-uint32_t pt_extend_blocks_per_cu(bool spill)
-{
-    int blocks = 0;
-    hipError_t e = hipErrorUnknown;
-    switch (pt_extend_variant()) {
-#define X(id, w, cap)                                                                                             \
-    case id:                                                                                                     \
-        e = spill ? hipOccupancyMaxActiveBlocksPerMultiprocessor(                                                \
-                        &blocks, ptd::extend_kernel<ptd::ray_source_slots, true, w, cap>, 256, 0)                \
-                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(                                                \
-                        &blocks, ptd::extend_kernel<ptd::ray_source_slots, false, w, cap>, 256, 0);              \
-        break;
-        PT_EXTEND_VARIANTS(X)
-#undef X
-    }
-    if (e != hipSuccess || blocks < 1) blocks = 1;
-    return (uint32_t)blocks;
 }

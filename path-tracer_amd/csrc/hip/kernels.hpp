@@ -47,17 +47,15 @@ struct dparams {
 
 hipError_t pt_launch_raygen(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
                             hipStream_t st);
-hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* counters,
-                            uint32_t* spill, uint32_t grid_blocks, hipStream_t st);
+hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* spill,
+                            hipStream_t st);
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
                            hipStream_t st);
 hipError_t pt_launch_xdiv_check(uint64_t n, uint32_t seed, unsigned long long* mismatches, hipStream_t st);
 hipError_t pt_launch_trace_rays(const ptd::dscene& S, uint32_t n, const float* origins, const uint32_t* vel,
-                                const float* dur, float4* hit, float2* hc, float4* rec, float2* uv, uint32_t* counters,
-                                uint32_t* spill, uint32_t grid_blocks, hipStream_t st);
+                                const float* dur, float4* hit, float2* hc, float4* rec, float2* uv, uint32_t* spill,
+                                hipStream_t st);
 hipError_t pt_launch_finalize(const ptd::dscene& S, uint32_t n, const float4* hit, const float2* hc, float4* rec,
                               float2* uv, hipStream_t st);
-uint32_t pt_extend_blocks_per_cu(bool spill);
 int pt_extend_variant();
 uint32_t pt_extend_stack_cap();
-uint32_t pt_extend_spill_threads(uint32_t grid_blocks, uint32_t n);

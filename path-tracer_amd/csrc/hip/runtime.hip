@@ -77,7 +77,6 @@ struct pt_device {
     int id = 0;
     hipStream_t stream = nullptr;
     uint32_t cu_count = 256;
-    uint32_t* counters = nullptr;     // 8 dequeue counters of the persistent extend kernel
     bool profiling = false;
     std::vector<event_pair> pending;
     std::vector<event_pair> free_events;
@@ -296,17 +295,14 @@ ptd::dparams Params(pt_basic_renderer* r, uint32_t seed)
     return P;
 }
 
-uint32_t ExtendGrid(pt_device* d, bool spill)
-{
-    return d->cu_count * pt_extend_blocks_per_cu(spill);
-}
-
-int EnsureSpill(pt_basic_renderer* r, uint32_t grid)
+// Traversal stack entries beyond the kernel's LDS capacity live in a global
+// buffer of (needed - capacity) rows x one column per ray.
+int EnsureSpill(pt_basic_renderer* r)
 {
     uint32_t need = r->scene->stack_needed, cap = pt_extend_stack_cap();
     if (need <= cap) { r->slots.spill = nullptr; return 0; }
     size_t rows = need - cap;
-    PT_HIP(r->spill.alloc(rows * (size_t)pt_extend_spill_threads(grid, r->slots.n)));
+    PT_HIP(r->spill.alloc(rows * (size_t)r->slots.n));
     r->slots.spill = r->spill.ptr;
     return 0;
 }
@@ -348,9 +344,8 @@ pt_device* ptCreateDevice(int hip_device)
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, hip_device) == hipSuccess && prop.multiProcessorCount > 0)
         d->cu_count = (uint32_t)prop.multiProcessorCount;
-    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&d->counters, 64) != hipSuccess) {
-        SetError("device stream / counter allocation failed");
+    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
+        SetError("device stream creation failed");
         if (d->stream) (void)hipStreamDestroy(d->stream);
         delete d;
         return nullptr;
@@ -365,7 +360,6 @@ void ptDestroyDevice(pt_device* d)
     (void)hipStreamSynchronize(d->stream);
     for (auto& ep : d->pending) { (void)hipEventDestroy(ep.a); (void)hipEventDestroy(ep.b); }
     for (auto& ep : d->free_events) { (void)hipEventDestroy(ep.a); (void)hipEventDestroy(ep.b); }
-    if (d->counters) (void)hipFree(d->counters);
     (void)hipStreamDestroy(d->stream);
     delete d;
 }
@@ -556,16 +550,14 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
     if (!d) { SetError("null device"); return -1; }
     if (CheckReady(r) != 0) return -1;
     PT_HIP(hipSetDevice(d->id));
-    bool spill = r->scene->stack_needed > pt_extend_stack_cap();
-    uint32_t grid = ExtendGrid(d, spill);
-    if (int e = EnsureSpill(r, grid)) return e;
+    if (int e = EnsureSpill(r)) return e;
     r->params.FrameIndex += 1;
     ptd::dparams P = Params(r, r->params.FrameIndex);
     ptd::dframe F = Frame(r);
     for (uint32_t i = 0; i < rounds; i++) {
         event_pair ep{};
         if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep)) return e;
-        PT_HIP(pt_launch_extend(r->scene->d, r->slots, F, d->counters, r->slots.spill, grid, d->stream));
+        PT_HIP(pt_launch_extend(r->scene->d, r->slots, F, r->slots.spill, d->stream));
         if (int e = EndTimed(d, ep)) return e;
         if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep)) return e;
         PT_HIP(pt_launch_shade(r->scene->d, r->slots, F, P, d->stream));
@@ -636,7 +628,6 @@ int ptTraceRays(pt_device* d, pt_scene* s, uint32_t n, const float* origins, con
     if (n == 0) return 0;
     PT_HIP(hipSetDevice(d->id));
     bool spill = s->stack_needed > pt_extend_stack_cap();
-    uint32_t grid = ExtendGrid(d, spill);
     dbuf<float> d_o, d_t;
     dbuf<uint32_t> d_v, d_spill;
     dbuf<float4> d_hit, d_rec;
@@ -648,9 +639,9 @@ int ptTraceRays(pt_device* d, pt_scene* s, uint32_t n, const float* origins, con
         if ((e = d_v.upload(vel, n)) != hipSuccess) break;
         if ((e = d_hit.alloc(n)) != hipSuccess || (e = d_rec.alloc(n)) != hipSuccess) break;
         if ((e = d_hc.alloc(n)) != hipSuccess || (e = d_uv.alloc(n)) != hipSuccess) break;
-        if (spill && (e = d_spill.alloc((size_t)(s->stack_needed - pt_extend_stack_cap()) * pt_extend_spill_threads(grid, n))) != hipSuccess) break;
+        if (spill && (e = d_spill.alloc((size_t)(s->stack_needed - pt_extend_stack_cap()) * n)) != hipSuccess) break;
         e = pt_launch_trace_rays(s->d, n, d_o.ptr, d_v.ptr, d_t.ptr, d_hit.ptr, d_hc.ptr, d_rec.ptr, d_uv.ptr,
-                                 d->counters, spill ? d_spill.ptr : nullptr, grid, d->stream);
+                                 spill ? d_spill.ptr : nullptr, d->stream);
         if (e != hipSuccess) break;
         if ((e = hipStreamSynchronize(d->stream)) != hipSuccess) break;
         std::vector<float4> rec(n);
