@@ -26,10 +26,11 @@ ROOT = Path(__file__).resolve().parent
 PKG_DIR = ROOT / "path-tracer_amd"
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# Algorithmic bytes per slot per launch (DESIGN.md "Roofline"): extend reads
-# the 16-B ray record and writes the 16-B hit record + 8-B UV; shade reads
-# ray 16 + hit 16 + uv 8 + path 56 and writes ray 16 + path 56.
-ALG_BYTES = {"extend": 40, "shade": 168}
+# Algorithmic bytes per ray per launch, SURVEY.md §8(d) (the reference's SoA
+# records, independent of this build's layout): extend reads the 20-B ray and
+# writes the 24-B hit; shade reads path 60 + ray/hit 44 and writes ray 20 +
+# path vertex 52.  Sum = the 220 B/ray whole-path figure.
+ALG_BYTES = {"extend": 44, "shade": 176}
 PATH_BYTES_PER_RAY = 220  # SURVEY.md §8(d) whole-path definition
 
 
@@ -189,7 +190,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (procedural 3,948-triangle room mesh + 1024^2 texture; Viking Room asset absent)",
+        "data": f"synthetic (procedural {info.mesh_face_count}-triangle room mesh + 1024^2 texture; "
+                "Viking Room asset absent)",
         "config": {
             "workload": f"C{args.config} room scene, {width}x{height} px ({info.width}x{info.height} per GPU), "
                         f"one round (extend+shade) per step, 16-row bands over {world} GPU(s)",

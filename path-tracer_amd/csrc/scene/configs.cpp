@@ -4,7 +4,7 @@
 //
 // The Viking Room OBJ and its texture are not available in this environment
 // (SURVEY.md §8(c) "Assets"), so C3/C4/C5 use a deterministic synthetic room
-// mesh of 3,948 triangles (two log walls, a plank floor, barrels, a chest, a
+// mesh of 3,976 triangles (two log walls, a plank floor, barrels, a chest, a
 // table, a bed and a pot) with a procedural 1024x1024 texture; C2's HDR sky
 // is procedural as well.  Every input is a pure function of this file.
 #include "scene.hpp"

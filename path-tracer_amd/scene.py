@@ -86,6 +86,10 @@ class Scene:
     def set_material(self, entity, material):
         N.scene_lib().ptsSetEntityMaterial(self._h, entity, material)
 
+    def shape_index(self, entity) -> int:
+        """Packed shape index of an entity after pack() (entity::PackedShapeIndex)."""
+        return int(N.scene_lib().ptsEntityPackedShapeIndex(entity))
+
     def set_mesh(self, entity, mesh):
         N.scene_lib().ptsSetEntityMesh(self._h, entity, mesh)
 

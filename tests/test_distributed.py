@@ -1,0 +1,56 @@
+"""Multi-rank path on CPU: world_size-2 gloo run of the band-partitioned
+render + frame-end sum reduce (the RCCL path of bench.py / ptCommReduce-
+SampleBuffer, with the CPU oracle standing in for the GPU renderer).  The
+reduced frame must equal the single-rank render bit for bit."""
+from __future__ import annotations
+
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+
+import oracle_lib
+
+HERE = Path(__file__).resolve().parent
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_two_rank_band_render_reduces_to_full_frame(pt, tmp_path):
+    cfg, W, H = 1, 48, 80          # 5 bands of 16 rows: rank 0 owns 3, rank 1 owns 2
+    out = tmp_path / "reduced.npz"
+    env = dict(os.environ, OMP_NUM_THREADS="2", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           str(HERE / "dist_worker.py"), str(out), str(cfg), str(W), str(H)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = np.load(out)
+    assert int(got["world"]) == 2
+    assert int(got["owned"][0]) == W * H           # bands cover the frame exactly once
+    s = pt.Scene.config(cfg)
+    o = oracle_lib.OracleRenderer(s.packs(), W, H, threads=2)
+    o.RenderFlags = 3
+    o.reset()
+    o.run(2)
+    o.run(1)
+    full = o.accum()
+    o.close()
+    s.close()
+    assert np.array_equal(got["accum"].view(np.uint32), full.view(np.uint32))
+
+
+def test_band_ownership(pt):
+    for H in (16, 80, 1080, 2160):
+        for N in (1, 2, 3, 8):
+            masks = [pt.owned_pixels(8, H, r, N) for r in range(N)]
+            assert np.array_equal(sum(m.astype(int) for m in masks), np.ones((H, 8), int))
+    rows = pt.band_rows(1080, 1, 8)
+    assert rows[0] == 16 and rows[15] == 31 and rows[16] == 16 * 9
