@@ -43,7 +43,19 @@ def load_package():
     return mod
 
 
-def cpu_baseline(pt, scene, width, height, max_seconds=12.0, max_rounds=6):
+def measured_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC profile
+    (profiles/traffic.json <- profiles/pmc_summary.py over separate
+    FETCH_SIZE / WRITE_SIZE passes of this bench, gfx950-corrected), or None."""
+    p = ROOT / "profiles" / "traffic.json"
+    if not p.exists():
+        return None, None
+    d = json.loads(p.read_text())
+    k = d.get("kernels", {}).get(kernel, {})
+    return k.get("hbm_bytes"), d.get("profile")
+
+
+def cpu_baseline(pt, scene, width, height, max_seconds=12.0, max_rounds=200):
     """Time the CPU oracle (scalar C++ restatement, std::thread over host
     cores) on the same scene and frame.  Bounded: Reset + Run(2) warm-up, then
     single rounds until max_seconds of timed work or max_rounds."""
@@ -178,6 +190,7 @@ def main():
     }
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
     achieved = kernels[dom]["gbps"]
+    traffic, traffic_src = measured_traffic(dom)
     out = {
         "metric": "Mrays/s (Viking Room 1920x1080, 1024spp)",
         "value": round(mrays, 3),
@@ -207,7 +220,10 @@ def main():
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 5),
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes per launch (HBM, PMC)",
+            "traffic_source": traffic_src,
+            "alg_bytes_per_launch": ALG_BYTES[dom] * slots_owned,
             "alg_bytes_per_slot": ALG_BYTES[dom],
             "launch_avg_ms": {"extend": round(avg_ext, 4), "shade": round(avg_sh, 4)},
             "path_gbps_220B_per_ray": round(PATH_BYTES_PER_RAY * rays / dt / 1e9, 2),

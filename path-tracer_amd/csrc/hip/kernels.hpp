@@ -25,7 +25,7 @@ struct dslots {
     float4* prob;       // probability[4]
     float4* smp;        // sample.xyz, normalized lambda0
     uint2* act;         // active-shape stack (2 x u16 pairs)
-    uint32_t* spill;    // traversal stack spill, rows x (persistent threads)
+    uint32_t* spill;    // traversal stack spill: (needed - LDS capacity) rows x n
     uint32_t n;
 };
 

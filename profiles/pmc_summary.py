@@ -1,16 +1,60 @@
-import csv, collections, sys, json
+"""Summarises rocprofv3 --pmc CSVs per kernel and derives HBM traffic.
+
+usage: python profiles/pmc_summary.py OUT_JSON counter_collection.csv [...]
+
+Per kernel: every counter summed over its dimensions within a dispatch, then
+averaged over dispatches.  HBM bytes per launch follow MI355X_MICROARCH.md
+§HBM: FETCH_SIZE and WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reports half
+the bytes of wide (16 B/lane) coalesced reads, so it is doubled; WRITE_SIZE is
+exact for 16-B/lane stores.  Both come from separate --pmc passes.
+"""
+import collections
+import csv
+import json
+import sys
+
+
 def load(path):
-    rows=list(csv.DictReader(open(path)))
-    per=collections.defaultdict(float); kn={}
-    for r in rows:
-        key=(r["Dispatch_Id"], r["Counter_Name"]); per[key]+=float(r["Counter_Value"]); kn[r["Dispatch_Id"]]=r["Kernel_Name"]
-    agg=collections.defaultdict(lambda: collections.defaultdict(list))
-    for (d,c),v in per.items(): agg[kn[d]][c].append(v)
-    return {k:{c:sum(v)/len(v) for c,v in d.items()} for k,d in agg.items()}
-out={}
-for p in sys.argv[1:]:
-    for k,d in load(p).items():
-        out.setdefault(k,{}).update(d)
-for k,d in out.items():
-    if "extend" in k or "shade" in k:
-        print(k, json.dumps({c: round(v,1) for c,v in d.items()}))
+    per = collections.defaultdict(float)
+    names = {}
+    for r in csv.DictReader(open(path)):
+        key = (r["Dispatch_Id"], r["Counter_Name"])
+        per[key] += float(r["Counter_Value"])
+        names[r["Dispatch_Id"]] = r["Kernel_Name"]
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
+    for (d, c), v in per.items():
+        agg[names[d]][c].append(v)
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in agg.items()}
+
+
+def short(name):
+    for k in ("extend", "shade", "raygen", "finalize"):
+        if f"{k}_kernel" in name:
+            return k
+    return name[:40]
+
+
+def main():
+    out_path, paths = sys.argv[1], sys.argv[2:]
+    kernels = {}
+    for p in paths:
+        for k, d in load(p).items():
+            kernels.setdefault(short(k), {}).update(d)
+    result = {}
+    for k, d in kernels.items():
+        e = {c: round(v, 1) for c, v in d.items()}
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            rd = 2.0 * d["FETCH_SIZE"] * 1024
+            wr = d["WRITE_SIZE"] * 1024
+            e["hbm_read_bytes"] = round(rd)
+            e["hbm_write_bytes"] = round(wr)
+            e["hbm_bytes"] = round(rd + wr)
+        if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d:
+            e["l2_hit_rate"] = round(d["TCC_HIT_sum"] / max(d["TCC_HIT_sum"] + d["TCC_MISS_sum"], 1), 4)
+        result[k] = e
+        print(k, json.dumps(e))
+    json.dump(result, open(out_path, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()
