@@ -129,6 +129,12 @@ int ptTraceRays(pt_device* device, pt_scene* scene, uint32_t n, const float* ori
  * returns the number of bit mismatches (must be 0). */
 int ptCheckFastDivision(pt_device* device, uint64_t n, uint32_t seed, uint64_t* mismatches);
 
+/* Diagnostic: runs the extend step on the renderer's current rays with
+ * traversal counters.  It writes the same hit records the next Run's extend
+ * writes first, so the render is not perturbed.  out = {rays, lane steps, wave steps x 64, internal nodes,
+ * BLAS leaves, faces tested, stack pops, TLAS leaves, waves}. */
+int ptExtendStats(pt_device* device, pt_basic_renderer* renderer, uint64_t out[9]);
+
 /* Per-kernel device time, measured with HIP events on the renderer stream. */
 int ptSetProfiling(pt_device* device, int enable);
 int ptGetKernelStats(pt_device* device, int kernel, uint64_t* launches, double* total_ms);

@@ -165,6 +165,7 @@ HIP_API = {
     "ptReadBasicRendererState": (_i32, [_vp, _vp, _vp]),
     "ptTraceRays": (_i32, [_vp, _vp, _u32, _fptr, _u32ptr, _fptr, _vp]),
     "ptCheckFastDivision": (_i32, [_vp, C.c_uint64, _u32, C.POINTER(C.c_uint64)]),
+    "ptExtendStats": (_i32, [_vp, _vp, C.POINTER(C.c_uint64)]),
     "ptSetProfiling": (_i32, [_vp, _i32]),
     "ptGetKernelStats": (_i32, [_vp, _i32, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
     "ptResetKernelStats": (_i32, [_vp]),

@@ -144,19 +144,41 @@ PT_DEV void LaneMeshFace(const dscene& S, uint32_t F, lane_state& L)
     L.C = v3(1 - U - W, U, W);
 }
 
+// Traversal statistics hooks: no-ops in the render kernel, counters in the
+// diagnostic instantiation (ptExtendStats).
+struct no_stats {
+    PT_DEV void step() {}
+    PT_DEV void internal() {}
+    PT_DEV void leaf(uint32_t) {}
+    PT_DEV void shape() {}
+    PT_DEV void pop() {}
+};
+struct lane_stats {
+    uint32_t steps = 0, internals = 0, leaves = 0, faces = 0, shapes = 0, pops = 0;
+    PT_DEV void step() { steps++; }
+    PT_DEV void internal() { internals++; }
+    PT_DEV void leaf(uint32_t n) { leaves++; faces += n; }
+    PT_DEV void shape() { shapes++; }
+    PT_DEV void pop() { pops++; }
+};
+
 // Advances one lane by one node.  Returns true when its Trace() is complete.
 // Only the two index words of the current node are carried between steps;
 // its bounds were already consumed by the parent's box test.
-template <bool SPILL, int CAP, class Src>
-PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, const Src& src, uint32_t slot)
+template <bool SPILL, int CAP, class Src, class Stats = no_stats>
+PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, const Src& src, uint32_t slot,
+                     Stats& ss)
 {
+    ss.step();
     const uint32_t* mesh_words = reinterpret_cast<const uint32_t*>(S.mesh_nodes);
     const uint32_t* shape_words = reinterpret_cast<const uint32_t*>(S.shape_nodes);
     if (L.blas != SHAPE_INDEX_NONE) {
         // IntersectMeshNode (scene.glsl.inc:336-399), one node.
         if (L.nb > 0) {
+            ss.leaf(L.nb - L.na);
             for (uint32_t F = L.na; F < L.nb; F++) LaneMeshFace(S, F, L);
         } else {
+            ss.internal();
             uint32_t Index = L.na;
             float4 a0 = S.mesh_nodes[2 * Index], a1 = S.mesh_nodes[2 * Index + 1];
             float4 b0 = S.mesh_nodes[2 * Index + 2], b1 = S.mesh_nodes[2 * Index + 3];
@@ -175,6 +197,7 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
             if (TA < PT_INFINITY) { L.na = __float_as_uint(a0.w); L.nb = __float_as_uint(a1.w); return false; }
         }
         if (L.dB > 0) {
+            ss.pop();
             uint32_t I = st.get(L.dT + --L.dB);
             L.na = mesh_words[8 * I + 3];
             L.nb = mesh_words[8 * I + 7];
@@ -192,6 +215,7 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
         // Intersect (scene.glsl.inc:468-520), one node.
         uint32_t Children = L.na;
         if (Children == 0) {
+            ss.shape();
             uint32_t ShapeIndex = L.nb;
             const pt_packed_shape* Shape = &S.shapes[ShapeIndex];
             const float* From = Shape->Transform.From;
@@ -211,6 +235,7 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
             }
             IntersectAnalytic(Type, O, V, ShapeIndex, L);
         } else {
+            ss.internal();
             uint32_t IA = Children & 0xFFFF, IB = Children >> 16;
             float4 a0 = S.shape_nodes[2 * IA], a1 = S.shape_nodes[2 * IA + 1];
             float4 b0 = S.shape_nodes[2 * IB], b1 = S.shape_nodes[2 * IB + 1];
@@ -230,6 +255,7 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
         }
     }
     if (L.dT > 0) {
+        ss.pop();
         uint32_t I = st.get(--L.dT);
         L.na = shape_words[8 * I + 3];
         L.nb = shape_words[8 * I + 7];
@@ -786,9 +812,54 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
     if (!src.load(slot, O, V, D)) return;
     lane_state Ln;
     LaneBegin(S, Ln, O, V, D);
+    no_stats ns;
     if (S.g.ShapeCount != 0)
-        while (!LaneStep<SPILL, CAP>(S, Ln, st, src, slot)) {}
+        while (!LaneStep<SPILL, CAP>(S, Ln, st, src, slot, ns)) {}
     src.store(slot, Ln);
+}
+
+PT_DEV uint32_t WaveSum(uint32_t v)
+{
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+PT_DEV uint32_t WaveMax(uint32_t v)
+{
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o, 64));
+    return v;
+}
+
+// Diagnostic extend: the same traversal with per-lane counters, reduced per
+// wave into out[]: {rays, lane steps, wave steps x 64, internal nodes, BLAS
+// leaves, faces tested, stack pops, TLAS leaves (shapes), waves}.  SIMD
+// efficiency of the traversal loop = lane steps / (wave steps x 64).
+template <class Src, bool SPILL, int CAP>
+__global__ __launch_bounds__(256) void extend_stats_kernel(dscene S, Src src, uint32_t n, uint32_t* spill,
+                                                           uint32_t spill_stride, unsigned long long* out)
+{
+    __shared__ uint32_t smem[CAP * 256];
+    uint32_t slot = blockIdx.x * 256 + threadIdx.x;
+    tstack<SPILL, CAP> st;
+    st.lds = &smem[threadIdx.x];
+    st.spill = spill + slot;
+    st.stride = spill_stride;
+    lane_stats ss;
+    pt3 O, V;
+    float D;
+    uint32_t ray = 0;
+    if (slot < n && src.load(slot, O, V, D)) {
+        ray = 1;
+        lane_state Ln;
+        LaneBegin(S, Ln, O, V, D);
+        if (S.g.ShapeCount != 0)
+            while (!LaneStep<SPILL, CAP>(S, Ln, st, src, slot, ss)) {}
+        src.store(slot, Ln);
+    }
+    uint32_t v[9] = {WaveSum(ray), WaveSum(ss.steps), WaveMax(ss.steps) * 64u, WaveSum(ss.internals),
+                     WaveSum(ss.leaves), WaveSum(ss.faces), WaveSum(ss.pops), WaveSum(ss.shapes), 1u};
+    if ((threadIdx.x & 63u) == 0)
+        for (int i = 0; i < 9; i++) atomicAdd(&out[i], (unsigned long long)v[i]);
 }
 
 // Compact hit -> the reference's packed trace record (StoreTraceHit,
@@ -957,6 +1028,22 @@ static hipError_t LaunchExtend(const ptd::dscene& S, const Src& src, uint32_t n,
         PT_EXTEND_VARIANTS(X)
 #undef X
     }
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_extend_stats(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* spill,
+                                  unsigned long long* out, hipStream_t st)
+{
+    if (L.n == 0) return hipSuccess;
+    ptd::ray_source_slots src{L, F};
+    constexpr int CAP = 20;
+    if (pt_extend_stack_cap() != CAP) return hipErrorInvalidConfiguration;
+    if (spill)
+        hipLaunchKernelGGL((ptd::extend_stats_kernel<ptd::ray_source_slots, true, CAP>), dim3(Blocks(L.n)), dim3(256),
+                           0, st, S, src, L.n, spill, L.n, out);
+    else
+        hipLaunchKernelGGL((ptd::extend_stats_kernel<ptd::ray_source_slots, false, CAP>), dim3(Blocks(L.n)),
+                           dim3(256), 0, st, S, src, L.n, spill, L.n, out);
     return hipGetLastError();
 }
 

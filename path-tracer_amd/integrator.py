@@ -174,6 +174,18 @@ class BasicRenderer:
     def run(self, rounds: int = 1):
         _check(N.hip_lib().ptRunBasicRenderer(self.device.handle, self._h, int(rounds)), "ptRunBasicRenderer")
 
+    def extend_stats(self) -> dict:
+        """Traversal counters of the current rays (diagnostic, ptExtendStats)."""
+        out = (C.c_uint64 * 9)()
+        _check(N.hip_lib().ptExtendStats(self.device.handle, self._h, out), "ptExtendStats")
+        keys = ("rays", "lane_steps", "wave_steps_x64", "internal_nodes", "blas_leaves", "faces", "pops",
+                "tlas_leaves", "waves")
+        d = dict(zip(keys, (int(x) for x in out)))
+        d["simd_efficiency"] = d["lane_steps"] / max(d["wave_steps_x64"], 1)
+        for k in ("lane_steps", "internal_nodes", "blas_leaves", "faces", "pops", "tlas_leaves"):
+            d[k + "_per_ray"] = d[k] / max(d["rays"], 1)
+        return d
+
     def read_state(self) -> np.ndarray:
         sb = self.sample_buffer
         out = np.zeros(sb.width * sb.height, dtype=N.PIXEL_STATE_DTYPE)

@@ -195,3 +195,29 @@ def test_fast_division_matches_ieee(pt, dev):
     """The extend kernel's FMA-corrected division is bit-identical to a / b."""
     for seed in (1, 2, 3, 4):
         assert dev.check_fast_division(1 << 28, seed) == 0
+
+
+def test_extend_stats_does_not_perturb(pt, dev):
+    """ptExtendStats traces the current rays (as the next Run's extend would),
+    so a render that calls it between rounds matches one that does not."""
+    s = scene_for(pt, 3)
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    out = []
+    for with_stats in (False, True):
+        sb = pt.SampleBuffer(dev, 96, 64)
+        r = pt.BasicRenderer(dev, ds, sb)
+        r.RenderFlags = 3
+        r.reset()
+        r.run(2)
+        if with_stats:
+            st = r.extend_stats()
+            assert st["rays"] == 96 * 64 and st["waves"] == 96 * 64 // 64
+            assert 0 < st["simd_efficiency"] <= 1.0
+            assert st["internal_nodes"] > 0 and st["faces"] >= st["blas_leaves"] > 0
+        r.run(1)
+        out.append((r.read_state(), sb.read()))
+        r.close(); sb.close()
+    assert np.array_equal(out[0][0].view(np.uint8), out[1][0].view(np.uint8))
+    assert np.array_equal(out[0][1].view(np.uint32), out[1][1].view(np.uint32))
+    ds.close()
