@@ -57,13 +57,20 @@ struct lane_state {
                          // BLAS {FaceBeginOrNodeIndex, FaceEndIndex}
     uint32_t dT, dB;     // TLAS / BLAS stack depths (<= 32 each)
     uint32_t blas;       // shape index of the mesh being traversed, NONE at TLAS level
+    bool exact;          // fast exact slab division applies to the current-level ray
 };
 
-PT_DEV void LaneBegin(const dscene& S, lane_state& L, pt3 O, pt3 V, float Duration)
+PT_DEV void SetLevelRay(const dscene& S, lane_state& L, pt3 O, pt3 V)
 {
     L.O = O;
     L.V = V;
-    L.Y = RecipForDiv3(V);
+    L.exact = S.fast_div && FastDivRay(O, V);
+    L.Y = v3(1.0f / V.x, 1.0f / V.y, 1.0f / V.z);
+}
+
+PT_DEV void LaneBegin(const dscene& S, lane_state& L, pt3 O, pt3 V, float Duration)
+{
+    SetLevelRay(S, L, O, V);
     L.Time = Duration;
     L.Shape = SHAPE_INDEX_NONE;
     L.Prim = 0;
@@ -182,8 +189,8 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
             uint32_t Index = L.na;
             float4 a0 = S.mesh_nodes[2 * Index], a1 = S.mesh_nodes[2 * Index + 1];
             float4 b0 = S.mesh_nodes[2 * Index + 2], b1 = S.mesh_nodes[2 * Index + 3];
-            float TA = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, a0, a1);
-            float TB = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, b0, b1);
+            float TA = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, a0, a1, L.exact);
+            float TB = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, b0, b1, L.exact);
             if (TA > TB) {
                 if (TA < PT_INFINITY && L.dB < 32) st.put(L.dT + L.dB++, Index);
                 L.na = __float_as_uint(b0.w); L.nb = __float_as_uint(b1.w);
@@ -208,9 +215,10 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
         if (L.Shape == 0xFFFFFFFEu) L.Shape = L.blas;
         L.blas = SHAPE_INDEX_NONE;
         if (L.dT == 0) return true;
+        pt3 WO, WV;
         float D;
-        src.load(slot, L.O, L.V, D);
-        L.Y = RecipForDiv3(L.V);
+        src.load(slot, WO, WV, D);
+        SetLevelRay(S, L, WO, WV);
     } else {
         // Intersect (scene.glsl.inc:468-520), one node.
         uint32_t Children = L.na;
@@ -224,9 +232,7 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
             int32_t Type = Shape->Type;
             if (Type == PT_SHAPE_TYPE_MESH_INSTANCE) {
                 uint32_t Root = Shape->MeshRootNodeIndex;
-                L.O = O;
-                L.V = V;
-                L.Y = RecipForDiv3(V);
+                SetLevelRay(S, L, O, V);
                 L.blas = ShapeIndex;
                 L.dB = 0;
                 L.na = mesh_words[8 * Root + 3];
@@ -239,8 +245,8 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
             uint32_t IA = Children & 0xFFFF, IB = Children >> 16;
             float4 a0 = S.shape_nodes[2 * IA], a1 = S.shape_nodes[2 * IA + 1];
             float4 b0 = S.shape_nodes[2 * IB], b1 = S.shape_nodes[2 * IB + 1];
-            float TA = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, a0, a1);
-            float TB = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, b0, b1);
+            float TA = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, a0, a1, L.exact);
+            float TB = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, b0, b1, L.exact);
             if (TA > TB) {
                 if (TA < PT_INFINITY && L.dT < 32) st.put(L.dT++, IA);
                 L.na = __float_as_uint(b0.w); L.nb = __float_as_uint(b1.w);

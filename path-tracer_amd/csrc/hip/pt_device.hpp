@@ -33,6 +33,7 @@ struct dscene {
     const pt_packed_camera* cameras;
     const float4* atlas;
     uint32_t atlas_w, atlas_h, atlas_layers;
+    uint32_t fast_div;             // every BVH box coordinate is 0 or in [2^-50, 2^40] (IntersectBoundingBox)
 };
 
 struct ray { pt3 Origin; pt3 Velocity; float Duration; };
@@ -141,21 +142,67 @@ PT_DEV float SlabEntry(pt3 MinT, pt3 MaxT, float Reach)
     return EntryT;
 }
 
-// Slab test (common.glsl.inc:153-185).  The six divisions by the ray velocity
-// use the exact fast quotient; if any of them leaves the range where that is
-// proven (rare: zero velocity components, extreme scales) the whole box is
-// recomputed with IEEE division.
-PT_DEV float IntersectBoundingBox(pt3 O, pt3 V, pt3 Y, float Reach, float4 MinAndX, float4 MaxAndX)
+// Exact fast slab test.  With y = RN(1/b), q = RN(a*y), r = fma(-q,b,a),
+// q' = fma(r,y,q) equals IEEE a/b whenever r is exact and q, r*y, q' stay
+// normal.  That holds for every plane of every box if
+//   * every box coordinate and ray-origin component is 0 or has magnitude in
+//     [2^-50, 2^40]  ->  every nonzero a = Min - O has |a| >= 2^-73, |a| <= 2^41
+//   * every ray-velocity component has magnitude in [2^-59, 2^27]
+// so |a/b| lies in [2^-100, 2^100] and r is exact (|a| >= 2^-103).  a = 0
+// gives q' = +-0, whose sign may differ from IEEE's; the slab test only
+// compares its quotients, where -0 == +0.  The box-coordinate condition is
+// checked once per scene on the host (dscene::fast_div), the ray condition
+// once per ray and traversal level (FastDivRay); rays outside it take the
+// IEEE path below.  No NaN reaches the fast path, so plain hardware min/max
+// (no IEEE-mode canonicalisation) give the same comparisons as fminf/fmaxf.
+PT_DEV bool FastDivRay(pt3 O, pt3 V)
+{
+    bool ok = true;
+#define PT_CHECK_O(c) { float m = pt_abs(c); ok &= (m == 0.0f) | ((m >= 0x1p-50f) & (m <= 0x1p40f)); }
+#define PT_CHECK_V(c) { float m = pt_abs(c); ok &= (m >= 0x1p-59f) & (m <= 0x1p27f); }
+    PT_CHECK_O(O.x) PT_CHECK_O(O.y) PT_CHECK_O(O.z)
+    PT_CHECK_V(V.x) PT_CHECK_V(V.y) PT_CHECK_V(V.z)
+#undef PT_CHECK_O
+#undef PT_CHECK_V
+    return ok;
+}
+
+PT_DEV float HwMin(float a, float b) { float r; asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
+PT_DEV float HwMax(float a, float b) { float r; asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
+PT_DEV float HwMin3(float a, float b, float c)
+{
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+PT_DEV float HwMax3(float a, float b, float c)
+{
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+PT_DEV float FastQuot(float a, float b, float y)
+{
+    float q = a * y;
+    float r = __builtin_fmaf(-q, b, a);
+    return __builtin_fmaf(r, y, q);
+}
+
+// Slab test (common.glsl.inc:153-185).  `exact`: the lane's ray satisfies
+// FastDivRay and the scene's boxes the coordinate condition.
+PT_DEV float IntersectBoundingBox(pt3 O, pt3 V, pt3 Y, float Reach, float4 MinAndX, float4 MaxAndX, bool exact)
 {
     pt3 A = xyz(MinAndX) - O, B = xyz(MaxAndX) - O;
-    bool bad = false;
-    pt3 MinT = v3(XDivNoGuard(A.x, V.x, Y.x, bad), XDivNoGuard(A.y, V.y, Y.y, bad), XDivNoGuard(A.z, V.z, Y.z, bad));
-    pt3 MaxT = v3(XDivNoGuard(B.x, V.x, Y.x, bad), XDivNoGuard(B.y, V.y, Y.y, bad), XDivNoGuard(B.z, V.z, Y.z, bad));
-    if (bad) {
-        MinT = A / V;
-        MaxT = B / V;
+    if (exact) {
+        float ax = FastQuot(A.x, V.x, Y.x), ay = FastQuot(A.y, V.y, Y.y), az = FastQuot(A.z, V.z, Y.z);
+        float bx = FastQuot(B.x, V.x, Y.x), by = FastQuot(B.y, V.y, Y.y), bz = FastQuot(B.z, V.z, Y.z);
+        float EntryT = HwMax3(HwMin(ax, bx), HwMin(ay, by), HwMin(az, bz));
+        float ExitT = HwMin3(HwMax(ax, bx), HwMax(ay, by), HwMax(az, bz));
+        bool miss = (ExitT < EntryT) | (ExitT <= 0.0f) | (EntryT >= Reach);
+        return miss ? PT_INFINITY : EntryT;
     }
-    return SlabEntry(MinT, MaxT, Reach);
+    return SlabEntry(A / V, B / V, Reach);
 }
 
 struct rng {

@@ -13,6 +13,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -390,6 +391,24 @@ void ptDestroyScene(pt_device* d, pt_scene* s)
 }
 
 // UpdateVulkanScene (scene.cpp:1692-2006): synchronous upload of the packs.
+// Box-coordinate condition of the extend kernel's exact fast slab division
+// (pt_device.hpp, IntersectBoundingBox): every TLAS / BLAS bound is 0 or has
+// magnitude in [2^-50, 2^40].  Scenes outside it trace with IEEE division.
+static bool FastDivBoxes(const pt_scene_packs* p)
+{
+    auto ok = [](float c) {
+        float m = std::fabs(c);
+        return m == 0.0f || (m >= 0x1p-50f && m <= 0x1p40f);
+    };
+    for (uint32_t i = 0; i < p->shape_node_count; i++)
+        for (int k = 0; k < 3; k++)
+            if (!ok(p->shape_nodes[i].Minimum[k]) || !ok(p->shape_nodes[i].Maximum[k])) return false;
+    for (uint32_t i = 0; i < p->mesh_node_count; i++)
+        for (int k = 0; k < 3; k++)
+            if (!ok(p->mesh_nodes[i].Minimum[k]) || !ok(p->mesh_nodes[i].Maximum[k])) return false;
+    return true;
+}
+
 int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t dirty)
 {
     if (!d || !s) { SetError("null device/scene"); return -1; }
@@ -429,6 +448,7 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     D.atlas_w = p->atlas_width;
     D.atlas_h = p->atlas_height;
     D.atlas_layers = p->atlas ? p->atlas_layer_count : 0;
+    D.fast_div = FastDivBoxes(p) ? 1u : 0u;
     s->camera_count = p->camera_count;
     s->stack_needed = need;
     s->valid = true;

@@ -51,6 +51,13 @@ def random_rays(arrays, n, seed):
         hi = np.minimum(hi, mx + 1.0)
     o = rng.uniform(lo, hi, size=(n, 3)).astype(np.float32)
     d = rng.normal(size=(n, 3))
+    # exercise the IEEE slab-division path: axis-aligned directions (zero
+    # velocity components), zero and tiny origin components
+    axes = np.array([[1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1],
+                     [0.6, 0.8, 0], [0, -0.6, 0.8], [1e-20, 1, 0.5]])
+    d[: 9 * 32] = np.repeat(axes, 32, axis=0)
+    o[64:128, 0] = 0.0
+    o[128:192, 1] = 1e-30
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     vel = oracle_lib.pack_unit_vectors(d.astype(np.float32))
     dur = np.full(n, 1048576.0, dtype=np.float32)
