@@ -493,9 +493,16 @@ PT_DEV bool Translucent_Sample(const dscene& S, rng& G, const bsdf_parameters& P
     return true;
 }
 
+// Material-type specialisation of the shade kernel: MATS is a superset of the
+// types referenced by the scene's shapes (computed on the host at upload), so
+// dispatch branches for absent types are compiled out without changing any
+// result.  PT_MATS_SCATTER: some medium can scatter (SceneScatterRate > 0 or
+// a translucent material exists).
+template <uint32_t MATS>
 PT_DEV void LoadMedium(const dscene& S, uint32_t M, pt4 Lambda, medium& Md)
 {
     Md.IOR = v4s(1.0f); Md.AbsorptionRate = v4s(0.0f); Md.ScatteringRate = v4s(0.0f); Md.ScatteringAnisotropy = 0.0f;
+    if (!(MATS & PT_MATS_TRANSLUCENT)) return;
     if (MUint(S, M, 0) != PT_MATERIAL_TYPE_BASIC_TRANSLUCENT) return;
     Md.IOR = CauchyEmpiricalIOR(MFloat(S, M, PT_BASIC_TRANSLUCENT_IOR), MFloat(S, M, PT_BASIC_TRANSLUCENT_ABBE_NUMBER), Lambda);
     float TD = MFloat(S, M, PT_BASIC_TRANSLUCENT_TRANSMISSION_DEPTH);
@@ -508,6 +515,7 @@ PT_DEV void LoadMedium(const dscene& S, uint32_t M, pt4 Lambda, medium& Md)
     }
 }
 
+template <uint32_t MATS>
 PT_DEV medium ResolveMedium(const dscene& S, uint32_t ShapeIndex, pt4 Lambda)
 {
     medium Md;
@@ -518,27 +526,29 @@ PT_DEV medium ResolveMedium(const dscene& S, uint32_t ShapeIndex, pt4 Lambda)
         Md.ScatteringRate = v4s(S.g.SceneScatterRate);
         Md.ScatteringAnisotropy = 0.0f;
     } else {
-        LoadMedium(S, S.shapes[ShapeIndex].MaterialIndex, Lambda, Md);
+        LoadMedium<MATS>(S, S.shapes[ShapeIndex].MaterialIndex, Lambda, Md);
         Md.Priority = ShapeIndex;
     }
     return Md;
 }
 
+template <uint32_t MATS>
 PT_DEV bool HasDirac(const dscene& S, const bsdf_parameters& P, uint32_t Type)
 {
-    if (Type == PT_MATERIAL_TYPE_BASIC_METAL)
+    if ((MATS & PT_MATS_METAL) && Type == PT_MATERIAL_TYPE_BASIC_METAL)
         return MaterialTexturableValue(S, P.MaterialIndex, PT_BASIC_METAL_ROUGHNESS, P.TextureUV) < 1e-3f;
-    if (Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT)
+    if ((MATS & PT_MATS_TRANSLUCENT) && Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT)
         return MaterialTexturableValue(S, P.MaterialIndex, PT_BASIC_TRANSLUCENT_ROUGHNESS, P.TextureUV) < 1e-3f;
     return false;
 }
 
 // SampleSurfaceIntegrand (basic_scatter.glsl:68-109)
+template <uint32_t MATS>
 PT_DEV bool SampleSurfaceIntegrand(const dscene& S, rng& G, pt3 Nrm, pt3 TX, pt3 TY, const bsdf_parameters& P, pt3 Out,
                                    pt3& In, pt4& Throughput, pt4& Probability)
 {
     uint32_t Type = MUint(S, P.MaterialIndex, 0);
-    float LightProbability = HasDirac(S, P, Type) ? 0.0f : S.g.SkyboxSamplingProbability;
+    float LightProbability = HasDirac<MATS>(S, P, Type) ? 0.0f : S.g.SkyboxSamplingProbability;
     pt4 MaterialPDF = v4s(0.0f);
     pt3 SMD = v3(S.g.SkyboxMeanDirection[0], S.g.SkyboxMeanDirection[1], S.g.SkyboxMeanDirection[2]);
     pt3 Mu = v3(dot(SMD, TX), dot(SMD, TY), dot(SMD, Nrm));
@@ -547,19 +557,22 @@ PT_DEV bool SampleSurfaceIntegrand(const dscene& S, rng& G, pt3 Nrm, pt3 TX, pt3
         In = RandomVonMisesFisher(G, S.g.SkyboxConcentration, Mu);
         if (In.z < 0.0f) return false;
         // MaterialEvaluateBSDF(Parameters, Out, In, ...)
-        if (Type == PT_MATERIAL_TYPE_BASIC_DIFFUSE) ok = Diffuse_Evaluate(S, P, Out, Throughput, MaterialPDF);
-        else if (Type == PT_MATERIAL_TYPE_BASIC_METAL) ok = Metal_Evaluate(S, P, Out, In, Throughput, MaterialPDF);
-        else if (Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT) ok = Translucent_Evaluate(S, P, Out, In, Throughput, MaterialPDF);
+        if ((MATS & PT_MATS_DIFFUSE) && Type == PT_MATERIAL_TYPE_BASIC_DIFFUSE)
+            ok = Diffuse_Evaluate(S, P, Out, Throughput, MaterialPDF);
+        else if ((MATS & PT_MATS_METAL) && Type == PT_MATERIAL_TYPE_BASIC_METAL)
+            ok = Metal_Evaluate(S, P, Out, In, Throughput, MaterialPDF);
+        else if ((MATS & PT_MATS_TRANSLUCENT) && Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT)
+            ok = Translucent_Evaluate(S, P, Out, In, Throughput, MaterialPDF);
         else ok = false;
         if (!ok) return false;
     } else {
         // MaterialSampleBSDF(Parameters, Out, In, ...)
-        if (Type == PT_MATERIAL_TYPE_BASIC_DIFFUSE) {
+        if ((MATS & PT_MATS_DIFFUSE) && Type == PT_MATERIAL_TYPE_BASIC_DIFFUSE) {
             In = SafeNormalize(RandomDirection(G) + v3(0, 0, 1));
             ok = Diffuse_Evaluate(S, P, Out, Throughput, MaterialPDF);
-        } else if (Type == PT_MATERIAL_TYPE_BASIC_METAL) {
+        } else if ((MATS & PT_MATS_METAL) && Type == PT_MATERIAL_TYPE_BASIC_METAL) {
             ok = Metal_Sample(S, G, P, Out, In, Throughput, MaterialPDF);
-        } else if (Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT) {
+        } else if ((MATS & PT_MATS_TRANSLUCENT) && Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT) {
             ok = Translucent_Sample(S, G, P, Out, In, Throughput, MaterialPDF);
         } else {
             ok = false;
@@ -642,6 +655,7 @@ PT_DEV void GenerateNewPath(const dscene& S, const dslots& L, const dframe& F, c
 
 // Scatter (basic_scatter.glsl:114-310).  Returns true if an extension ray was
 // produced (written to O, V).
+template <uint32_t MATS>
 PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3& V, uint32_t HitShape,
                     uint32_t HitMaterial, float HitTime, uint32_t PN, uint32_t PT, pt2 UV)
 {
@@ -654,11 +668,13 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
     uint32_t Active = SHAPE_INDEX_NONE;
     for (int I = 0; I < 4; I++) Active = pt_umin(Active, Path.Active[I]);
 
-    medium Md = ResolveMedium(S, Active, Lambda);
-    Path.Throughput = Path.Throughput * vexp(-Md.AbsorptionRate * HitTime);
+    medium Md = ResolveMedium<MATS>(S, Active, Lambda);
+    // Without translucent materials every medium is vacuum: exp(-0 * t) = 1
+    // exactly, so the multiply is an identity and is skipped.
+    if (MATS & PT_MATS_TRANSLUCENT) Path.Throughput = Path.Throughput * vexp(-Md.AbsorptionRate * HitTime);
 
     float ScatteringTime = PT_HIT_TIME_LIMIT;
-    if (Md.ScatteringRate.x > 0.0f) ScatteringTime = -pt_log(G.R01()) / Md.ScatteringRate.x;
+    if ((MATS & PT_MATS_SCATTER) && Md.ScatteringRate.x > 0.0f) ScatteringTime = -pt_log(G.R01()) / Md.ScatteringRate.x;
 
     if (HitTime >= ScatteringTime) {
         if (ScatteringTime < PT_HIT_TIME_LIMIT) {
@@ -705,7 +721,7 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
                 if (Path.Active[I] == Active) continue;
                 Ext = pt_umin(Ext, Path.Active[I]);
             }
-            ExteriorIOR = ResolveMedium(S, Ext, Lambda).IOR;
+            ExteriorIOR = ResolveMedium<MATS>(S, Ext, Lambda).IOR;
         }
     }
 
@@ -717,7 +733,7 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
         P.Lambda = Lambda;
         P.ExteriorIOR = ExteriorIOR;
         pt4 T, Pr;
-        if (!SampleSurfaceIntegrand(S, G, Nrm, TX, TY, P, Out, In, T, Pr)) return false;
+        if (!SampleSurfaceIntegrand<MATS>(S, G, Nrm, TX, TY, P, Out, In, T, Pr)) return false;
         float Scale = 1.0f / pt_max(PT_EPSILON, max4(Pr));
         Path.Throughput = Path.Throughput * (T * Scale);
         Path.Probability = Path.Probability * (Pr * Scale);
@@ -725,13 +741,21 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
         In = -Out;
     }
 
+    // Active-shape stack update (basic_scatter.glsl:266-282): first free slot
+    // on entry, first matching slot on exit; constant indices keep the four
+    // slots in registers.
     if (In.z * Out.z < 0) {
+        uint32_t* A = Path.Active;
         if (Out.z > 0) {
-            for (int I = 0; I < 4; I++)
-                if (Path.Active[I] == SHAPE_INDEX_NONE) { Path.Active[I] = HitShape; break; }
+            if (A[0] == SHAPE_INDEX_NONE) A[0] = HitShape;
+            else if (A[1] == SHAPE_INDEX_NONE) A[1] = HitShape;
+            else if (A[2] == SHAPE_INDEX_NONE) A[2] = HitShape;
+            else if (A[3] == SHAPE_INDEX_NONE) A[3] = HitShape;
         } else {
-            for (int I = 0; I < 4; I++)
-                if (Path.Active[I] == HitShape) { Path.Active[I] = SHAPE_INDEX_NONE; break; }
+            if (A[0] == HitShape) A[0] = SHAPE_INDEX_NONE;
+            else if (A[1] == HitShape) A[1] = SHAPE_INDEX_NONE;
+            else if (A[2] == HitShape) A[2] = SHAPE_INDEX_NONE;
+            else if (A[3] == HitShape) A[3] = SHAPE_INDEX_NONE;
         }
     }
 
@@ -893,7 +917,9 @@ __global__ __launch_bounds__(256) void finalize_kernel(dscene S, uint32_t n, con
     uv[i] = make_float2(UV.x, UV.y);
 }
 
-__global__ __launch_bounds__(256) void shade_kernel(dscene S, dslots L, dframe F, dparams Pm)
+template <uint32_t MATS>
+__global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? 5 : 1) void shade_kernel(dscene S, dslots L, dframe F,
+                                                                                    dparams Pm)
 {
     uint32_t s = blockIdx.x * 256 + threadIdx.x;
     if (s >= L.n) return;
@@ -938,7 +964,7 @@ __global__ __launch_bounds__(256) void shade_kernel(dscene S, dslots L, dframe F
         PTg = PackUnitVector(TX);
     }
 
-    if (Scatter(S, G, Pm.termination_probability, P, O, V, HitShape, HitMaterial, HitTime, PN, PTg, UV)) {
+    if (Scatter<MATS>(S, G, Pm.termination_probability, P, O, V, HitShape, HitMaterial, HitTime, PN, PTg, UV)) {
         StoreRay(L, s, O, V);
         StorePathVertex(L, s, P);
     } else {
@@ -1059,11 +1085,31 @@ hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const pt
     return LaunchExtend(S, ptd::ray_source_slots{L, F}, L.n, spill, st);
 }
 
+// Shade instantiations by material-type mask: the smallest superset of the
+// scene's mask is launched.
+uint32_t pt_shade_mats(uint32_t scene_mats)
+{
+    if ((scene_mats & ~(uint32_t)PT_MATS_DIFFUSE) == 0) return PT_MATS_DIFFUSE;
+    if ((scene_mats & ~(uint32_t)(PT_MATS_DIFFUSE | PT_MATS_METAL)) == 0) return PT_MATS_DIFFUSE | PT_MATS_METAL;
+    return PT_MATS_ALL;
+}
+
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
-                           hipStream_t st)
+                           uint32_t scene_mats, hipStream_t st)
 {
     if (L.n == 0) return hipSuccess;
-    hipLaunchKernelGGL(ptd::shade_kernel, dim3(Blocks(L.n)), dim3(256), 0, st, S, L, F, P);
+    switch (pt_shade_mats(scene_mats)) {
+    case PT_MATS_DIFFUSE:
+        hipLaunchKernelGGL(ptd::shade_kernel<PT_MATS_DIFFUSE>, dim3(Blocks(L.n)), dim3(256), 0, st, S, L, F, P);
+        break;
+    case PT_MATS_DIFFUSE | PT_MATS_METAL:
+        hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_DIFFUSE | PT_MATS_METAL>), dim3(Blocks(L.n)), dim3(256), 0, st,
+                           S, L, F, P);
+        break;
+    default:
+        hipLaunchKernelGGL(ptd::shade_kernel<PT_MATS_ALL>, dim3(Blocks(L.n)), dim3(256), 0, st, S, L, F, P);
+        break;
+    }
     return hipGetLastError();
 }
 

@@ -51,8 +51,17 @@ hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const pt
                             hipStream_t st);
 hipError_t pt_launch_extend_stats(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* spill,
                                   unsigned long long* out, hipStream_t st);
+// Material-type mask of a scene (shade kernel specialisation).
+enum : uint32_t {
+    PT_MATS_DIFFUSE = 1,
+    PT_MATS_METAL = 2,
+    PT_MATS_TRANSLUCENT = 4,
+    PT_MATS_SCATTER = 8,
+    PT_MATS_ALL = 15,
+};
+uint32_t pt_shade_mats(uint32_t scene_mats);
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
-                           hipStream_t st);
+                           uint32_t scene_mats, hipStream_t st);
 hipError_t pt_launch_xdiv_check(uint64_t n, uint32_t seed, unsigned long long* mismatches, hipStream_t st);
 hipError_t pt_launch_trace_rays(const ptd::dscene& S, uint32_t n, const float* origins, const uint32_t* vel,
                                 const float* dur, float4* hit, float2* hc, float4* rec, float2* uv, uint32_t* spill,

@@ -99,6 +99,7 @@ struct pt_scene {
     dbuf<float> atlas;
     uint32_t camera_count = 0;
     uint32_t stack_needed = 0;   // max traversal stack entries (TLAS + BLAS)
+    uint32_t mats = PT_MATS_ALL; // material types referenced by shapes (shade specialisation)
     bool valid = false;
 };
 
@@ -409,6 +410,21 @@ static bool FastDivBoxes(const pt_scene_packs* p)
     return true;
 }
 
+// Material types reachable by a hit (every shape's material) plus whether any
+// medium can scatter: selects the shade kernel instantiation (kernels.hip).
+static uint32_t SceneMaterialMask(const pt_scene_packs* p)
+{
+    uint32_t m = 0;
+    for (uint32_t i = 0; i < p->shape_count; i++) {
+        uint32_t type = p->material_data[32 * p->shapes[i].MaterialIndex];
+        if (type == PT_MATERIAL_TYPE_BASIC_DIFFUSE) m |= PT_MATS_DIFFUSE;
+        else if (type == PT_MATERIAL_TYPE_BASIC_METAL) m |= PT_MATS_METAL;
+        else if (type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT) m |= PT_MATS_TRANSLUCENT;
+    }
+    if ((m & PT_MATS_TRANSLUCENT) || p->globals->SceneScatterRate > 0.0f) m |= PT_MATS_SCATTER;
+    return m;
+}
+
 int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t dirty)
 {
     if (!d || !s) { SetError("null device/scene"); return -1; }
@@ -449,6 +465,7 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     D.atlas_h = p->atlas_height;
     D.atlas_layers = p->atlas ? p->atlas_layer_count : 0;
     D.fast_div = FastDivBoxes(p) ? 1u : 0u;
+    s->mats = SceneMaterialMask(p);
     s->camera_count = p->camera_count;
     s->stack_needed = need;
     s->valid = true;
@@ -580,7 +597,7 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
         PT_HIP(pt_launch_extend(r->scene->d, r->slots, F, r->slots.spill, d->stream));
         if (int e = EndTimed(d, ep)) return e;
         if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep)) return e;
-        PT_HIP(pt_launch_shade(r->scene->d, r->slots, F, P, d->stream));
+        PT_HIP(pt_launch_shade(r->scene->d, r->slots, F, P, r->scene->mats, d->stream));
         if (int e = EndTimed(d, ep)) return e;
     }
     return 0;

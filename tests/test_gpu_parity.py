@@ -228,3 +228,34 @@ def test_extend_stats_does_not_perturb(pt, dev):
     assert np.array_equal(out[0][0].view(np.uint8), out[1][0].view(np.uint8))
     assert np.array_equal(out[0][1].view(np.uint32), out[1][1].view(np.uint32))
     ds.close()
+
+
+def test_diffuse_metal_scene_bit_exact(pt, dev):
+    """A scene with only diffuse + metal materials runs the diffuse|metal shade
+    instantiation; it must match the oracle like the full one."""
+    s = pt.Scene.create()
+    m1 = s.create_material(pt.MATERIAL_BASIC_METAL, "Rough", BaseColor=(0.9, 0.6, 0.3), Roughness=0.3)
+    m2 = s.create_material(pt.MATERIAL_BASIC_METAL, "Mirror", BaseColor=(0.8, 0.8, 0.9), Roughness=0.0)
+    # CreateScene's camera sits at (0,0,1) looking down at the plane
+    s.create_entity(pt.ENTITY_SPHERE, position=(0.5, 0.2, 0.35), scale=(0.3, 0.3, 0.3), material=m1)
+    s.create_entity(pt.ENTITY_CUBE, position=(-0.6, -0.3, 0.2), scale=(0.2, 0.2, 0.2), material=m2)
+    s.set_root(skybox_sampling_probability=0.3)
+    s.pack()
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    W, H = 64, 48
+    sb = pt.SampleBuffer(dev, W, H)
+    r = pt.BasicRenderer(dev, ds, sb)
+    o = oracle_lib.OracleRenderer(s.packs(), W, H)
+    for x in (r, o):
+        x.RenderFlags = 3
+        x.reset()
+        x.run(2)
+        x.run(1)
+        x.run(1)
+    dev.synchronize()
+    compare_state(r.read_state(), o.state())
+    assert np.array_equal(sb.read().view(np.uint32), o.accum().view(np.uint32))
+    for x in (r, sb, ds):
+        x.close()
+    s.close()
