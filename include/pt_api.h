@@ -14,6 +14,8 @@
  *   ptDestroyBasicRenderer    src/integrator/basic.hpp:29  DestroyBasicRenderer
  *   ptResetBasicRenderer      src/integrator/basic.hpp:31  ResetBasicRenderer
  *   ptRunBasicRenderer        src/integrator/basic.hpp:32  RunBasicRenderer
+ *   ptRenderSampleBuffer      src/integrator/integrator.hpp:55-60  RenderSampleBuffer
+ *                             (resolve.glsl: XYZ -> sRGB, tone mapping)
  *   ptBasicRendererParams     src/integrator/basic.hpp:6-26  (the caller-written
  *                             CameraIndex / RenderFlags / PathLengthLimit /
  *                             PathTerminationProbability fields, FrameIndex)
@@ -84,11 +86,26 @@ typedef struct pt_pixel_state {
 } pt_pixel_state;
 
 enum {
-    PT_KERNEL_RAYGEN = 0,
-    PT_KERNEL_EXTEND = 1,
-    PT_KERNEL_SHADE  = 2,
-    PT_KERNEL_COUNT  = 3,
+    PT_KERNEL_RAYGEN  = 0,
+    PT_KERNEL_EXTEND  = 1,
+    PT_KERNEL_SHADE   = 2,
+    PT_KERNEL_RESOLVE = 3,
+    PT_KERNEL_COUNT   = 4,
 };
+
+/* resolve_parameters (src/integrator/integrator.hpp:12-48). */
+enum {
+    PT_TONE_MAPPING_CLAMP    = 0,
+    PT_TONE_MAPPING_REINHARD = 1,
+    PT_TONE_MAPPING_HABLE    = 2,
+    PT_TONE_MAPPING_ACES     = 3,
+};
+
+typedef struct pt_resolve_parameters {
+    float    Brightness;                  /* default 1 */
+    uint32_t ToneMappingMode;             /* PT_TONE_MAPPING_*, default CLAMP */
+    float    ToneMappingWhiteLevel;       /* Reinhard white level, default 1 */
+} pt_resolve_parameters;
 
 const char* ptGetLastError(void);
 
@@ -105,6 +122,17 @@ pt_sample_buffer* ptCreateSampleBuffer(pt_device* device, uint32_t width, uint32
 void              ptDestroySampleBuffer(pt_device* device, pt_sample_buffer* buffer);
 /* rgba = width*height*4 floats: CIE XYZ sums + sample count, row-major. */
 int               ptReadSampleBuffer(pt_device* device, pt_sample_buffer* buffer, float* rgba);
+/* Overwrites the accumulator (e.g. to resume accumulation from a saved one). */
+int               ptWriteSampleBuffer(pt_device* device, pt_sample_buffer* buffer, const float* rgba);
+/* RenderSampleBuffer: resolves the accumulator into the buffer's display
+ * image on the device stream (resolve.glsl:112-128). */
+int               ptRenderSampleBuffer(pt_device* device, pt_sample_buffer* buffer, const pt_resolve_parameters* params);
+/* Display image of the last ptRenderSampleBuffer: the fragment shader's
+ * OutColor (rgba32f, alpha 1) ... */
+int               ptReadResolvedImage(pt_device* device, pt_sample_buffer* buffer, float* rgba);
+/* ... and its 8-bit sRGB encoding as a B8G8R8A8_SRGB swapchain stores it
+ * (bytes R,G,B,A per pixel). */
+int               ptReadResolvedImageSRGB8(pt_device* device, pt_sample_buffer* buffer, uint8_t* rgba8);
 
 pt_basic_renderer* ptCreateBasicRenderer(pt_device* device, pt_scene* scene, pt_sample_buffer* buffer);
 /* Renderer owning only the 16-row pixel bands b with b % nranks == rank. */

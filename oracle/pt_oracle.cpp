@@ -1270,6 +1270,92 @@ void oracle_trace_rays(const pt_scene_packs* packs, uint32_t n, const float* ori
     }
 }
 
+// --- resolve.glsl (RenderSampleBuffer) -----------------------------------------
+
+namespace {
+
+float Luminance(pt3 C) { return dot(C, v3(0.2126f, 0.7152f, 0.0722f)); }                       // resolve.glsl:61-64
+
+pt3 Mat3TimesVec3(const float (&M)[3][3], pt3 V)   // GLSL mat3 * vec3, M[column][row]
+{
+    return v3(M[0][0] * V.x + M[1][0] * V.y + M[2][0] * V.z,
+              M[0][1] * V.x + M[1][1] * V.y + M[2][1] * V.z,
+              M[0][2] * V.x + M[1][2] * V.y + M[2][2] * V.z);
+}
+
+pt3 ToneMapReinhard(pt3 Color, float WhiteLevel)                                                // :66-73
+{
+    float OldL = Luminance(Color);
+    float MaxL = WhiteLevel;
+    float N = OldL * (1.0f + (OldL / (MaxL * MaxL)));
+    float NewL = N / (1.0f + OldL);
+    return Color * NewL / OldL;
+}
+
+pt3 ToneMapHablePartial(pt3 X)                                                                  // :75-80
+{
+    float A = 0.15f, B = 0.50f, C = 0.10f;
+    float D = 0.20f, E = 0.02f, F = 0.30f;
+    return ((X * (A * X + v3s(C * B)) + v3s(D * E)) / (X * (A * X + v3s(B)) + v3s(D * F))) - v3s(E / F);
+}
+
+pt3 ToneMapHable(pt3 Color)                                                                     // :82-89
+{
+    float ExposureBias = 2.0f;
+    pt3 Current = ToneMapHablePartial(Color * ExposureBias);
+    pt3 W = v3s(11.2f);
+    pt3 WhiteScale = v3s(1.0f) / ToneMapHablePartial(W);
+    return Current * WhiteScale;
+}
+
+const float ACES_INPUT_MATRIX[3][3] = {{0.59719f, 0.07600f, 0.02840f},                          // :91-96
+                                       {0.35458f, 0.90834f, 0.13383f},
+                                       {0.04823f, 0.01566f, 0.83777f}};
+const float ACES_OUTPUT_MATRIX[3][3] = {{1.60475f, -0.10208f, -0.00327f},                       // :98-103
+                                        {-0.53108f, 1.10813f, -0.07276f},
+                                        {-0.07367f, -0.00605f, 1.07602f}};
+const float CIE_XYZ_TO_SRGB[3][3] = {{+3.2406f, -0.9689f, +0.0557f},                            // spectrum.glsl.inc:50-55
+                                     {-1.5372f, +1.8758f, -0.2040f},
+                                     {-0.4986f, +0.0415f, +1.0570f}};
+
+pt3 ToneMapACES(pt3 Color)                                                                      // :105-111
+{
+    pt3 V = Mat3TimesVec3(ACES_INPUT_MATRIX, Color);
+    pt3 A = V * (V + v3s(0.0245786f)) - v3s(0.000090537f);
+    pt3 B = V * (0.983729f * V + v3s(0.4329510f)) + v3s(0.238081f);
+    return Mat3TimesVec3(ACES_OUTPUT_MATRIX, A / B);
+}
+
+// sRGB transfer + UNORM8 quantisation of a B8G8R8A8_SRGB store (vulkan.cpp:1407)
+// under the build's convention (pt_exp/pt_log power, round half up).
+uint8_t EncodeSRGB8(float C)
+{
+    C = pt_clamp(C, 0.0f, 1.0f);
+    float E = C <= 0.0031308f ? 12.92f * C : 1.055f * pt_exp(pt_log(C) * (1.0f / 2.4f)) - 0.055f;
+    return (uint8_t)(uint32_t)(pt_clamp(E, 0.0f, 1.0f) * 255.0f + 0.5f);
+}
+
+}  // namespace
+
+void oracle_resolve(const float* accum, uint32_t n, const pt_resolve_parameters* P, float* out, uint8_t* out8)
+{
+    for (uint32_t i = 0; i < n; i++) {                                                          // main, :113-130
+        const float* Value = accum + 4 * (size_t)i;
+        pt3 Color = v3s(0.0f);
+        if (Value[3] > 0)
+            Color = Mat3TimesVec3(CIE_XYZ_TO_SRGB, P->Brightness * v3(Value[0], Value[1], Value[2]) / Value[3]);
+        if (P->ToneMappingMode == PT_TONE_MAPPING_CLAMP)
+            Color = v3(pt_clamp(Color.x, 0.0f, 1.0f), pt_clamp(Color.y, 0.0f, 1.0f), pt_clamp(Color.z, 0.0f, 1.0f));
+        if (P->ToneMappingMode == PT_TONE_MAPPING_REINHARD) Color = ToneMapReinhard(Color, P->ToneMappingWhiteLevel);
+        if (P->ToneMappingMode == PT_TONE_MAPPING_HABLE) Color = ToneMapHable(Color);
+        if (P->ToneMappingMode == PT_TONE_MAPPING_ACES) Color = ToneMapACES(Color);
+        float* O = out + 4 * (size_t)i;
+        O[0] = Color.x; O[1] = Color.y; O[2] = Color.z; O[3] = 1.0f;
+        uint8_t* O8 = out8 + 4 * (size_t)i;
+        O8[0] = EncodeSRGB8(Color.x); O8[1] = EncodeSRGB8(Color.y); O8[2] = EncodeSRGB8(Color.z); O8[3] = 255;
+    }
+}
+
 float oracle_fp_exp(float x) { return pt_exp(x); }
 float oracle_fp_log(float x) { return pt_log(x); }
 float oracle_fp_sin(float x) { return pt_sin(x); }

@@ -39,6 +39,10 @@ void oracle_counters(oracle_renderer* r, uint64_t* rays, uint64_t* samples);
 void oracle_trace_rays(const pt_scene_packs* packs, uint32_t n, const float* origins,
                        const uint32_t* packed_velocities, const float* durations, pt_hit_record* out);
 
+/* RenderSampleBuffer (resolve.glsl:60-130) of n accumulator pixels:
+ * out = OutColor (rgba32f), out8 = sRGB8 swapchain bytes (R,G,B,A). */
+void oracle_resolve(const float* accum, uint32_t n, const pt_resolve_parameters* params, float* out, uint8_t* out8);
+
 /* Convention kernels, exposed for known-answer tests. */
 float oracle_fp_exp(float x);
 float oracle_fp_log(float x);

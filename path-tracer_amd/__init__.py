@@ -10,9 +10,11 @@ from .scene import (Scene, spectrum_coefficients, build_spectrum_table, load_spe
                     ENTITY_SPHERE, ENTITY_CUBE, MATERIAL_BASIC_DIFFUSE, MATERIAL_BASIC_METAL,
                     MATERIAL_BASIC_TRANSLUCENT, MATERIAL_OPENPBR, TEXTURE_RAW, TEXTURE_REFLECTANCE_WITH_ALPHA,
                     TEXTURE_RADIANCE, SCENE_DIRTY_ALL, RENDER_FLAG_ACCUMULATE, RENDER_FLAG_SAMPLE_JITTER)
-from .integrator import (Device, DeviceScene, SampleBuffer, BasicRenderer, Comm, PathTracerError, device_count,
-                         CreateSampleBuffer, CreateBasicRenderer, ResetBasicRenderer, RunBasicRenderer,
-                         DestroyBasicRenderer, DestroySampleBuffer)
+from .integrator import (Device, DeviceScene, SampleBuffer, BasicRenderer, Comm, PathTracerError, ResolveParameters,
+                         device_count, CreateSampleBuffer, CreateBasicRenderer, ResetBasicRenderer, RunBasicRenderer,
+                         DestroyBasicRenderer, DestroySampleBuffer, RenderSampleBuffer)
+from ._native import TONE_MAPPING_CLAMP, TONE_MAPPING_REINHARD, TONE_MAPPING_HABLE, TONE_MAPPING_ACES
+from .image import write_png, write_ppm, write_pfm, read_png
 from .layout import band_rows, owned_pixels
 
 __all__ = [n for n in dir() if not n.startswith("_")]

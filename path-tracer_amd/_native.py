@@ -49,6 +49,15 @@ class pt_basic_renderer_params(C.Structure):
     ]
 
 
+class pt_resolve_parameters(C.Structure):
+    """resolve_parameters (src/integrator/integrator.hpp:43-48)."""
+    _fields_ = [
+        ("Brightness", C.c_float),
+        ("ToneMappingMode", C.c_uint32),
+        ("ToneMappingWhiteLevel", C.c_float),
+    ]
+
+
 class pts_config_info(C.Structure):
     _fields_ = [
         ("width", C.c_uint32), ("height", C.c_uint32), ("spp", C.c_uint32), ("camera_count", C.c_uint32),
@@ -96,7 +105,8 @@ assert SHAPE_NODE_DTYPE.itemsize == 32 and MESH_NODE_DTYPE.itemsize == 32 and ME
 assert SHAPE_DTYPE.itemsize == 144 and CAMERA_DTYPE.itemsize == 160 and GLOBALS_DTYPE.itemsize == 48
 assert TEXTURE_DTYPE.itemsize == 32
 
-KERNEL_RAYGEN, KERNEL_EXTEND, KERNEL_SHADE = 0, 1, 2
+KERNEL_RAYGEN, KERNEL_EXTEND, KERNEL_SHADE, KERNEL_RESOLVE = 0, 1, 2, 3
+TONE_MAPPING_CLAMP, TONE_MAPPING_REINHARD, TONE_MAPPING_HABLE, TONE_MAPPING_ACES = 0, 1, 2, 3
 
 _vp = C.c_void_p
 _u32 = C.c_uint32
@@ -155,6 +165,10 @@ HIP_API = {
     "ptCreateSampleBuffer": (_vp, [_vp, _u32, _u32]),
     "ptDestroySampleBuffer": (None, [_vp, _vp]),
     "ptReadSampleBuffer": (_i32, [_vp, _vp, _fptr]),
+    "ptWriteSampleBuffer": (_i32, [_vp, _vp, _fptr]),
+    "ptRenderSampleBuffer": (_i32, [_vp, _vp, C.POINTER(pt_resolve_parameters)]),
+    "ptReadResolvedImage": (_i32, [_vp, _vp, _fptr]),
+    "ptReadResolvedImageSRGB8": (_i32, [_vp, _vp, C.POINTER(C.c_uint8)]),
     "ptCreateBasicRenderer": (_vp, [_vp, _vp, _vp]),
     "ptCreateBasicRendererPartitioned": (_vp, [_vp, _vp, _vp, _u32, _u32]),
     "ptDestroyBasicRenderer": (None, [_vp, _vp]),

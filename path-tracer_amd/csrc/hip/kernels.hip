@@ -169,6 +169,27 @@ struct lane_stats {
     PT_DEV void pop() { pops++; }
 };
 
+// BLAS stack entries.  When the scene allows (dscene::blas_words, checked on
+// the host) an entry is the pushed node's own index words, packed: leaf ->
+// 1<<31 | count<<26 | first face (count <= 31, first face < 2^26); internal ->
+// child-pair index (< 2^31).  A pop is then an LDS read only.  Otherwise the
+// entry is the node index and a pop reloads its words (two global loads).
+PT_DEV uint32_t PackBlasEntry(uint32_t w0, uint32_t w1)
+{
+    return w1 > 0 ? (0x80000000u | ((w1 - w0) << 26) | w0) : w0;
+}
+
+PT_DEV void UnpackBlasEntry(uint32_t e, uint32_t& na, uint32_t& nb)
+{
+    if (e >> 31) {
+        na = e & 0x03FFFFFFu;
+        nb = na + ((e >> 26) & 31u);
+    } else {
+        na = e;
+        nb = 0;
+    }
+}
+
 // Advances one lane by one node.  Returns true when its Trace() is complete.
 // Only the two index words of the current node are carried between steps;
 // its bounds were already consumed by the parent's box test.
@@ -192,12 +213,16 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
             float TA = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, a0, a1, L.exact);
             float TB = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, b0, b1, L.exact);
             if (TA > TB) {
-                if (TA < PT_INFINITY && L.dB < 32) st.put(L.dT + L.dB++, Index);
+                if (TA < PT_INFINITY && L.dB < 32)
+                    st.put(L.dT + L.dB++, S.blas_words ? PackBlasEntry(__float_as_uint(a0.w), __float_as_uint(a1.w))
+                                                       : Index);
                 L.na = __float_as_uint(b0.w); L.nb = __float_as_uint(b1.w);
                 return false;
             }
             if (TB < PT_INFINITY) {
-                if (L.dB < 32) st.put(L.dT + L.dB++, Index + 1);
+                if (L.dB < 32)
+                    st.put(L.dT + L.dB++, S.blas_words ? PackBlasEntry(__float_as_uint(b0.w), __float_as_uint(b1.w))
+                                                       : Index + 1);
                 L.na = __float_as_uint(a0.w); L.nb = __float_as_uint(a1.w);
                 return false;
             }
@@ -205,9 +230,13 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
         }
         if (L.dB > 0) {
             ss.pop();
-            uint32_t I = st.get(L.dT + --L.dB);
-            L.na = mesh_words[8 * I + 3];
-            L.nb = mesh_words[8 * I + 7];
+            uint32_t E = st.get(L.dT + --L.dB);
+            if (S.blas_words) {
+                UnpackBlasEntry(E, L.na, L.nb);
+            } else {
+                L.na = mesh_words[8 * E + 3];
+                L.nb = mesh_words[8 * E + 7];
+            }
             return false;
         }
         // IntersectMeshNode returned (scene.glsl.inc:409-411); back to the

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "../../../include/pt_packed.h"
+#include "../../../include/pt_api.h"
 
 // Traversal-stack entries kept in LDS per thread (TLAS + BLAS combined);
 // deeper entries go to a per-slot global spill area (only allocated when the
@@ -60,6 +61,8 @@ enum : uint32_t {
     PT_MATS_ALL = 15,
 };
 uint32_t pt_shade_mats(uint32_t scene_mats);
+hipError_t pt_launch_resolve(const float4* accum, uint32_t n, float brightness, uint32_t mode, float white, float4* out,
+                             uint32_t* out8, hipStream_t st);
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
                            uint32_t scene_mats, hipStream_t st);
 hipError_t pt_launch_xdiv_check(uint64_t n, uint32_t seed, unsigned long long* mismatches, hipStream_t st);

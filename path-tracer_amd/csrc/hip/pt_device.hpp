@@ -34,6 +34,7 @@ struct dscene {
     const float4* atlas;
     uint32_t atlas_w, atlas_h, atlas_layers;
     uint32_t fast_div;             // every BVH box coordinate is 0 or in [2^-50, 2^40] (IntersectBoundingBox)
+    uint32_t blas_words;           // BLAS stack holds packed node words (PackBlasEntry, kernels.hip)
 };
 
 struct ray { pt3 Origin; pt3 Velocity; float Duration; };

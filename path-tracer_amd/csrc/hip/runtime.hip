@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -107,6 +108,9 @@ struct pt_sample_buffer {
     pt_device* dev = nullptr;
     uint32_t width = 0, height = 0;
     float4* accum = nullptr;
+    dbuf<float4> display;      // resolved image (ptRenderSampleBuffer)
+    dbuf<uint32_t> display8;   // its sRGB8 encoding
+    bool resolved = false;
 };
 
 struct pt_basic_renderer {
@@ -410,6 +414,26 @@ static bool FastDivBoxes(const pt_scene_packs* p)
     return true;
 }
 
+// Whether every BLAS node's index words fit one packed stack entry
+// (PackBlasEntry): leaves with <= 31 faces starting below 2^26, child-pair
+// indices below 2^31.  PT_BLAS_WORDS=0 forces the index form (A/B testing).
+static bool BlasWordsPackable(const pt_scene_packs* p)
+{
+    const char* e = getenv("PT_BLAS_WORDS");
+    if (e && atoi(e) == 0) return false;
+    for (uint32_t i = 0; i < p->mesh_node_count; i++) {
+        const pt_packed_mesh_node& n = p->mesh_nodes[i];
+        if (n.FaceEndIndex > 0) {
+            if (n.FaceBeginOrNodeIndex >= (1u << 26) || n.FaceEndIndex < n.FaceBeginOrNodeIndex ||
+                n.FaceEndIndex - n.FaceBeginOrNodeIndex > 31)
+                return false;
+        } else if (n.FaceBeginOrNodeIndex >= 0x80000000u) {
+            return false;
+        }
+    }
+    return true;
+}
+
 // Material types reachable by a hit (every shape's material) plus whether any
 // medium can scatter: selects the shade kernel instantiation (kernels.hip).
 static uint32_t SceneMaterialMask(const pt_scene_packs* p)
@@ -466,6 +490,7 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     D.atlas_layers = p->atlas ? p->atlas_layer_count : 0;
     D.fast_div = FastDivBoxes(p) ? 1u : 0u;
     s->mats = SceneMaterialMask(p);
+    D.blas_words = BlasWordsPackable(p) ? 1u : 0u;
     s->camera_count = p->camera_count;
     s->stack_needed = need;
     s->valid = true;
@@ -495,6 +520,8 @@ void ptDestroySampleBuffer(pt_device* d, pt_sample_buffer* b)
     if (!b) return;
     if (d) (void)hipSetDevice(d->id);
     if (b->accum) (void)hipFree(b->accum);
+    b->display.release();
+    b->display8.release();
     delete b;
 }
 
@@ -503,6 +530,54 @@ int ptReadSampleBuffer(pt_device* d, pt_sample_buffer* b, float* rgba)
     if (!d || !b || !rgba) { SetError("null argument"); return -1; }
     PT_HIP(hipSetDevice(d->id));
     PT_HIP(hipMemcpyAsync(rgba, b->accum, (size_t)b->width * b->height * sizeof(float4), hipMemcpyDeviceToHost, d->stream));
+    PT_HIP(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+int ptWriteSampleBuffer(pt_device* d, pt_sample_buffer* b, const float* rgba)
+{
+    if (!d || !b || !rgba) { SetError("null argument"); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    PT_HIP(hipMemcpyAsync(b->accum, rgba, (size_t)b->width * b->height * sizeof(float4), hipMemcpyHostToDevice, d->stream));
+    PT_HIP(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+// RenderSampleBuffer (integrator.cpp:105-159 + resolve.glsl:112-128)
+int ptRenderSampleBuffer(pt_device* d, pt_sample_buffer* b, const pt_resolve_parameters* p)
+{
+    if (!d || !b || !p) { SetError("null argument"); return -1; }
+    if (p->ToneMappingMode > PT_TONE_MAPPING_ACES) { SetError("bad tone mapping mode %u", p->ToneMappingMode); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    size_t n = (size_t)b->width * b->height;
+    PT_HIP(b->display.alloc(n));
+    PT_HIP(b->display8.alloc(n));
+    event_pair ep{};
+    if (int e = BeginTimed(d, PT_KERNEL_RESOLVE, ep)) return e;
+    PT_HIP(pt_launch_resolve(b->accum, (uint32_t)n, p->Brightness, p->ToneMappingMode, p->ToneMappingWhiteLevel,
+                             b->display.ptr, b->display8.ptr, d->stream));
+    if (int e = EndTimed(d, ep)) return e;
+    b->resolved = true;
+    return 0;
+}
+
+int ptReadResolvedImage(pt_device* d, pt_sample_buffer* b, float* rgba)
+{
+    if (!d || !b || !rgba) { SetError("null argument"); return -1; }
+    if (!b->resolved) { SetError("sample buffer not resolved (call ptRenderSampleBuffer)"); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    PT_HIP(hipMemcpyAsync(rgba, b->display.ptr, (size_t)b->width * b->height * sizeof(float4), hipMemcpyDeviceToHost,
+                          d->stream));
+    PT_HIP(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+int ptReadResolvedImageSRGB8(pt_device* d, pt_sample_buffer* b, uint8_t* rgba8)
+{
+    if (!d || !b || !rgba8) { SetError("null argument"); return -1; }
+    if (!b->resolved) { SetError("sample buffer not resolved (call ptRenderSampleBuffer)"); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    PT_HIP(hipMemcpyAsync(rgba8, b->display8.ptr, (size_t)b->width * b->height * 4, hipMemcpyDeviceToHost, d->stream));
     PT_HIP(hipStreamSynchronize(d->stream));
     return 0;
 }

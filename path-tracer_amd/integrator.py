@@ -109,6 +109,19 @@ class DeviceScene:
             self._h = None
 
 
+class ResolveParameters:
+    """resolve_parameters (integrator.hpp:43-48) with the reference defaults."""
+
+    def __init__(self, Brightness: float = 1.0, ToneMappingMode: int = N.TONE_MAPPING_CLAMP,
+                 ToneMappingWhiteLevel: float = 1.0):
+        self.Brightness = float(Brightness)
+        self.ToneMappingMode = int(ToneMappingMode)
+        self.ToneMappingWhiteLevel = float(ToneMappingWhiteLevel)
+
+    def as_struct(self) -> N.pt_resolve_parameters:
+        return N.pt_resolve_parameters(self.Brightness, self.ToneMappingMode, self.ToneMappingWhiteLevel)
+
+
 class SampleBuffer:
     """rgba32f accumulator: CIE XYZ sums + sample count (integrator.cpp:15-87)."""
 
@@ -127,6 +140,30 @@ class SampleBuffer:
     def read(self) -> np.ndarray:
         out = np.zeros((self.height, self.width, 4), dtype=np.float32)
         _check(N.hip_lib().ptReadSampleBuffer(self.device.handle, self._h, N.fptr(out)), "ptReadSampleBuffer")
+        return out
+
+    def write(self, rgba: np.ndarray):
+        """Overwrite the accumulator (resume accumulation from a saved one)."""
+        a = np.ascontiguousarray(rgba, dtype=np.float32).reshape(self.height, self.width, 4)
+        _check(N.hip_lib().ptWriteSampleBuffer(self.device.handle, self._h, N.fptr(a)), "ptWriteSampleBuffer")
+
+    def render(self, params: "ResolveParameters | None" = None, **kw):
+        """RenderSampleBuffer (integrator.hpp:55-60): resolve on the device."""
+        p = (params or ResolveParameters(**kw)).as_struct()
+        _check(N.hip_lib().ptRenderSampleBuffer(self.device.handle, self._h, C.byref(p)), "ptRenderSampleBuffer")
+
+    def read_resolved(self) -> np.ndarray:
+        """OutColor of the last render(): (H, W, 4) float32, alpha 1."""
+        out = np.zeros((self.height, self.width, 4), dtype=np.float32)
+        _check(N.hip_lib().ptReadResolvedImage(self.device.handle, self._h, N.fptr(out)), "ptReadResolvedImage")
+        return out
+
+    def read_srgb8(self) -> np.ndarray:
+        """The resolved image as B8G8R8A8_SRGB stores it: (H, W, 4) uint8, RGBA order."""
+        out = np.zeros((self.height, self.width, 4), dtype=np.uint8)
+        _check(N.hip_lib().ptReadResolvedImageSRGB8(self.device.handle, self._h,
+                                                    out.ctypes.data_as(C.POINTER(C.c_uint8))),
+               "ptReadResolvedImageSRGB8")
         return out
 
     def close(self):
@@ -250,3 +287,7 @@ def DestroyBasicRenderer(device: Device, renderer: BasicRenderer):
 
 def DestroySampleBuffer(device: Device, sample_buffer: SampleBuffer):
     sample_buffer.close()
+
+
+def RenderSampleBuffer(device: Device, sample_buffer: SampleBuffer, parameters: ResolveParameters):
+    sample_buffer.render(parameters)

@@ -259,3 +259,25 @@ def test_diffuse_metal_scene_bit_exact(pt, dev):
     for x in (r, sb, ds):
         x.close()
     s.close()
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_resolve_bit_exact(pt, dev, mode):
+    """RenderSampleBuffer on the device vs the oracle: OutColor and sRGB8."""
+    rng = np.random.default_rng(mode)
+    W, H = 96, 40
+    acc = rng.uniform(0, 4, size=(H, W, 4)).astype(np.float32)
+    acc[..., 3] = rng.integers(0, 50, size=(H, W)).astype(np.float32)
+    acc[0, :8] = 0
+    acc[1, :8, :3] *= -1
+    acc[2, :8, :3] *= 1e6
+    sb = pt.SampleBuffer(dev, W, H)
+    sb.write(acc)
+    assert np.array_equal(sb.read(), acc)
+    sb.render(pt.ResolveParameters(Brightness=1.7, ToneMappingMode=mode, ToneMappingWhiteLevel=3.0))
+    out, out8 = sb.read_resolved(), sb.read_srgb8()
+    ref, ref8 = oracle_lib.resolve(acc, 1.7, mode, 3.0)
+    same = (out.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(out) & np.isnan(ref))
+    assert same.all(), np.argwhere(~same)[:5]
+    assert np.array_equal(out8, ref8)
+    sb.close()
