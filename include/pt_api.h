@@ -16,6 +16,10 @@
  *   ptRunBasicRenderer        src/integrator/basic.hpp:32  RunBasicRenderer
  *   ptRenderSampleBuffer      src/integrator/integrator.hpp:55-60  RenderSampleBuffer
  *                             (resolve.glsl: XYZ -> sRGB, tone mapping)
+ *   ptCreatePreviewRenderContext  src/application/preview_render.hpp:65-70
+ *   ptDestroyPreviewRenderContext preview_render.hpp:72-76
+ *   ptRenderPreview           preview_render.hpp:85-90  RenderPreview
+ *   ptRetrievePreviewQueryResult  preview_render.hpp:78-83
  *   ptBasicRendererParams     src/integrator/basic.hpp:6-26  (the caller-written
  *                             CameraIndex / RenderFlags / PathLengthLimit /
  *                             PathTerminationProbability fields, FrameIndex)
@@ -46,6 +50,7 @@ typedef struct pt_scene pt_scene;
 typedef struct pt_sample_buffer pt_sample_buffer;
 typedef struct pt_basic_renderer pt_basic_renderer;
 typedef struct pt_comm pt_comm;
+typedef struct pt_preview pt_preview;
 
 /* Mutable renderer state (src/integrator/basic.hpp:18-25).  The caller writes
  * CameraIndex, RenderFlags, PathLengthLimit and PathTerminationProbability
@@ -90,7 +95,8 @@ enum {
     PT_KERNEL_EXTEND  = 1,
     PT_KERNEL_SHADE   = 2,
     PT_KERNEL_RESOLVE = 3,
-    PT_KERNEL_COUNT   = 4,
+    PT_KERNEL_PREVIEW = 4,
+    PT_KERNEL_COUNT   = 5,
 };
 
 /* resolve_parameters (src/integrator/integrator.hpp:12-48). */
@@ -100,6 +106,41 @@ enum {
     PT_TONE_MAPPING_HABLE    = 2,
     PT_TONE_MAPPING_ACES     = 3,
 };
+
+/* preview_render_mode (src/application/preview_render.hpp:3-13). */
+enum {
+    PT_PREVIEW_RENDER_MODE_BASE_COLOR        = 0,
+    PT_PREVIEW_RENDER_MODE_BASE_COLOR_SHADED = 1,
+    PT_PREVIEW_RENDER_MODE_NORMAL            = 2,
+    PT_PREVIEW_RENDER_MODE_MATERIAL_INDEX    = 3,
+    PT_PREVIEW_RENDER_MODE_PRIMITIVE_INDEX   = 4,
+    PT_PREVIEW_RENDER_MODE_MESH_COMPLEXITY   = 5,
+    PT_PREVIEW_RENDER_MODE_SCENE_COMPLEXITY  = 6,
+};
+
+/* preview_parameters (preview_render.hpp:22-33). */
+typedef struct pt_preview_parameters {
+    pt_packed_transform CameraTransform;
+    uint32_t RenderMode;
+    float    Brightness;
+    uint32_t SelectedShapeIndex;          /* 0xFFFFFFFF = none */
+    uint32_t RenderSizeX, RenderSizeY;
+    uint32_t MouseX, MouseY;
+} pt_preview_parameters;
+
+/* Per-pixel primary-hit AOVs of the preview: Trace()'s hit (scene.glsl.inc:
+ * 102-119) for the pixel's primary ray. */
+typedef struct pt_preview_aov {
+    float    time;
+    uint32_t shape_index;                 /* 0xFFFFFFFF on a miss (other fields 0) */
+    uint32_t material_index;
+    uint32_t primitive_index;
+    uint32_t mesh_complexity;             /* BLAS nodes visited (Hit.MeshComplexity) */
+    uint32_t scene_complexity;            /* TLAS nodes visited (Hit.SceneComplexity) */
+    float    normal[3];                   /* world normal, not quantised */
+    float    u, v;
+    uint32_t reserved;
+} pt_preview_aov;
 
 typedef struct pt_resolve_parameters {
     float    Brightness;                  /* default 1 */
@@ -146,6 +187,20 @@ uint32_t           ptBasicRendererSlotCount(pt_basic_renderer* renderer);
 /* out = width*height states in image order; pixels outside the renderer's
  * partition are left untouched. */
 int                ptReadBasicRendererState(pt_device* device, pt_basic_renderer* renderer, pt_pixel_state* out);
+
+/* Editor preview (preview_render.glsl:96-178): one primary ray per pixel of
+ * RenderSizeX x RenderSizeY through the same Trace() as the integrator.
+ * RenderPreview enqueues; the reads synchronise.  The query result is the
+ * shape index under (MouseX, MouseY) of the last render (0xFFFFFFFF = sky or
+ * no render yet; a mouse position outside the image leaves it unchanged, as
+ * the reference's query buffer). */
+pt_preview* ptCreatePreviewRenderContext(pt_device* device, pt_scene* scene);
+void        ptDestroyPreviewRenderContext(pt_device* device, pt_preview* context);
+int         ptRenderPreview(pt_device* device, pt_preview* context, const pt_preview_parameters* params);
+int         ptRetrievePreviewQueryResult(pt_device* device, pt_preview* context, uint32_t* hit_shape_index);
+/* rgba: RenderSizeX * RenderSizeY * 4 floats (OutColor); aov: one record per pixel. */
+int         ptReadPreviewImage(pt_device* device, pt_preview* context, float* rgba);
+int         ptReadPreviewAOVs(pt_device* device, pt_preview* context, pt_preview_aov* aov);
 
 /* Bit-exact Trace() (scene.glsl.inc:522-611) of n rays: origins (3n floats),
  * packed unit velocities (n), durations (n) -> n hit records. */

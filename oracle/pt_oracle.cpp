@@ -7,6 +7,7 @@
 // velocity / normal / tangent, 16-bit active-shape stack), because that
 // quantisation is part of the algorithm's observable behaviour.
 #include "pt_oracle.h"
+#include "../include/pt_cie.h"
 #include "../include/pt_glsl.h"
 
 #include <atomic>
@@ -1354,6 +1355,152 @@ void oracle_resolve(const float* accum, uint32_t n, const pt_resolve_parameters*
         uint8_t* O8 = out8 + 4 * (size_t)i;
         O8[0] = EncodeSRGB8(Color.x); O8[1] = EncodeSRGB8(Color.y); O8[2] = EncodeSRGB8(Color.z); O8[3] = 255;
     }
+}
+
+// --- preview_render.glsl (RenderPreview) ----------------------------------------
+
+namespace {
+
+const float D65[PT_CIE_D65_COUNT] = {PT_CIE_D65_VALUES};                                         // spectrum.glsl.inc:56-157
+
+float SampleIlluminantD65(float NormalizedLambda)                                               // :159-164
+{
+    float Offset = NormalizedLambda * 470;
+    int Index = (int)Offset;
+    Index = Index < 0 ? 0 : (Index > 469 ? 469 : Index);
+    return pt_mix(D65[Index], D65[Index + 1], Offset - (float)Index);
+}
+
+float SampleParametricSpectrumI(pt4 BetaAndIntensity, float Lambda)                            // :183-186
+{
+    return BetaAndIntensity.w * SampleParametricSpectrum(v3(BetaAndIntensity.x, BetaAndIntensity.y, BetaAndIntensity.z), Lambda);
+}
+
+pt3 ObserveParametricSpectrumUnderD65(pt4 BetaAndIntensity)                                     // :194-208
+{
+    const int SampleCount = 16;
+    const float DeltaLambda = (PT_CIE_LAMBDA_MAX - PT_CIE_LAMBDA_MIN) / SampleCount;
+    pt3 Color = v3s(0);
+    for (int I = 0; I < SampleCount; I++) {
+        float NormalizedLambda = (float)I / (float)(SampleCount - 1);
+        float D = SampleIlluminantD65(NormalizedLambda) / PT_CIE_D65_NORMALIZATION;
+        float Lambda = pt_mix(PT_CIE_LAMBDA_MIN, PT_CIE_LAMBDA_MAX, NormalizedLambda);
+        Color = Color + SampleParametricSpectrumI(BetaAndIntensity, Lambda) * D * SampleStandardObserver(Lambda) * DeltaLambda;
+    }
+    return Color;
+}
+
+pt3 ObserveBetaUnderD65(pt3 Beta) { return ObserveParametricSpectrumUnderD65(v4(Beta.x, Beta.y, Beta.z, 1)); }   // :210-213
+
+const float PREVIEW_COLORS[20][3] = {                                                           // preview_render.glsl:16-38
+    {0.902f, 0.098f, 0.294f}, {0.235f, 0.706f, 0.294f}, {1.000f, 0.882f, 0.098f}, {0.263f, 0.388f, 0.847f},
+    {0.961f, 0.510f, 0.192f}, {0.569f, 0.118f, 0.706f}, {0.275f, 0.941f, 0.941f}, {0.941f, 0.196f, 0.902f},
+    {0.737f, 0.965f, 0.047f}, {0.980f, 0.745f, 0.745f}, {0.000f, 0.502f, 0.502f}, {0.902f, 0.745f, 1.000f},
+    {0.604f, 0.388f, 0.141f}, {1.000f, 0.980f, 0.784f}, {0.502f, 0.000f, 0.000f}, {0.667f, 1.000f, 0.765f},
+    {0.502f, 0.502f, 0.000f}, {1.000f, 0.847f, 0.694f}, {0.000f, 0.000f, 0.459f}, {0.502f, 0.502f, 0.502f}};
+
+pt3 PreviewColor(uint32_t I) { return v3(PREVIEW_COLORS[I % 20][0], PREVIEW_COLORS[I % 20][1], PREVIEW_COLORS[I % 20][2]); }
+
+struct preview_context {
+    const context& C;
+
+    pt3 MaterialColor(uint32_t M, uint32_t A) const                                             // scene.glsl.inc:254-258
+    {
+        return ObserveBetaUnderD65(C.MaterialVec3(M, A));
+    }
+
+    pt3 MaterialTexturableColor(uint32_t M, uint32_t A, pt2 UV) const                           // :260-274
+    {
+        pt3 Color = ObserveBetaUnderD65(C.MaterialVec3(M, A + 0));
+        uint32_t TextureIndex = C.MaterialUint(M, A + 3);
+        if (TextureIndex != TEXTURE_INDEX_NONE) {
+            pt4 T = C.SampleTexture(TextureIndex, UV);
+            Color = Color * ObserveBetaUnderD65(v3(T.x, T.y, T.z));
+        }
+        return Color;
+    }
+
+    pt3 MaterialBaseColor(uint32_t M, pt2 UV) const                                             // :696-701 + *_BaseColor
+    {
+        uint32_t Type = C.MaterialType(M);
+        if (Type == PT_MATERIAL_TYPE_BASIC_DIFFUSE) return MaterialTexturableColor(M, PT_BASIC_DIFFUSE_BASE_SPECTRUM, UV);
+        if (Type == PT_MATERIAL_TYPE_BASIC_METAL) return MaterialTexturableColor(M, PT_BASIC_METAL_BASE_SPECTRUM, UV);
+        if (Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT) return MaterialColor(M, PT_BASIC_TRANSLUCENT_TRANSMISSION_SPECTRUM);
+        return v3s(0);
+    }
+};
+
+}  // namespace
+
+void oracle_preview(const pt_scene_packs* packs, const pt_preview_parameters* P, float* rgba, pt_preview_aov* aov,
+                    uint32_t* hit_shape_index)
+{
+    scene_data S(packs);
+    context C(S);
+    preview_context PC{C};
+    const uint32_t W = P->RenderSizeX, H = P->RenderSizeY;
+    for (uint32_t Py = 0; Py < H; Py++)
+        for (uint32_t Px = 0; Px < W; Px++) {                                                   // main, :96-178
+            // ScreenXY interpolated at the pixel centre of a W x H viewport
+            pt2 ScreenXY = v2(((float)Px + 0.5f) / (float)W, ((float)Py + 0.5f) / (float)H);
+            float AspectRatio = (float)W / (float)H;
+            float NearX = (ScreenXY.x - 0.5f) * AspectRatio;
+            float NearY = 0.5f - ScreenXY.y;
+            ray Ray;
+            Ray.Origin = v3s(0);
+            Ray.Velocity = normalize(v3(NearX, NearY, -1.0f));
+            Ray.Duration = PT_HIT_TIME_LIMIT;
+            Ray = TransformRay(Ray, P->CameraTransform);
+            hit Hit = C.Trace(Ray);
+            pt3 Color = v3s(0);
+            bool Miss = Hit.ShapeIndex == SHAPE_INDEX_NONE;
+            switch (P->RenderMode) {
+            case PT_PREVIEW_RENDER_MODE_BASE_COLOR:
+            case PT_PREVIEW_RENDER_MODE_BASE_COLOR_SHADED:
+                if (Miss) {
+                    Color = Mat3TimesVec3(CIE_XYZ_TO_SRGB, ObserveParametricSpectrumUnderD65(C.SampleSkyboxSpectrum(Ray.Velocity)));
+                } else {
+                    Color = Mat3TimesVec3(CIE_XYZ_TO_SRGB, PC.MaterialBaseColor(Hit.MaterialIndex, Hit.UV));
+                    if (P->RenderMode == PT_PREVIEW_RENDER_MODE_BASE_COLOR_SHADED)
+                        Color = Color * dot(Hit.Normal, -Ray.Velocity);
+                }
+                break;
+            case PT_PREVIEW_RENDER_MODE_NORMAL:
+                Color = Miss ? 0.5f * (v3s(1) - Ray.Velocity) : 0.5f * (Hit.Normal + v3s(1));
+                break;
+            case PT_PREVIEW_RENDER_MODE_MATERIAL_INDEX:
+                if (!Miss) Color = PreviewColor(Hit.MaterialIndex);
+                break;
+            case PT_PREVIEW_RENDER_MODE_PRIMITIVE_INDEX:
+                if (!Miss) Color = PreviewColor(Hit.PrimitiveIndex);
+                break;
+            case PT_PREVIEW_RENDER_MODE_MESH_COMPLEXITY:
+                Color = v3(0, 1, 0) * (float)Hit.MeshComplexity / 256.0f;
+                break;
+            case PT_PREVIEW_RENDER_MODE_SCENE_COMPLEXITY:
+                Color = v3(0, 1, 0) * (float)Hit.SceneComplexity / 256.0f;
+                break;
+            }
+            if (Hit.ShapeIndex == P->SelectedShapeIndex) Color = Color * v3(1.0f, 0.5f, 0.5f);
+            Color = Color * P->Brightness;
+            if (hit_shape_index && Px == P->MouseX && Py == P->MouseY) *hit_shape_index = Hit.ShapeIndex;
+            size_t i = (size_t)Py * W + Px;
+            if (rgba) { rgba[4 * i] = Color.x; rgba[4 * i + 1] = Color.y; rgba[4 * i + 2] = Color.z; rgba[4 * i + 3] = 1.0f; }
+            if (aov) {
+                pt_preview_aov& A = aov[i];
+                std::memset(&A, 0, sizeof(A));
+                A.shape_index = Hit.ShapeIndex;
+                A.mesh_complexity = Hit.MeshComplexity;
+                A.scene_complexity = Hit.SceneComplexity;
+                if (!Miss) {
+                    A.time = Hit.Time;
+                    A.material_index = Hit.MaterialIndex;
+                    A.primitive_index = Hit.PrimitiveIndex;
+                    A.normal[0] = Hit.Normal.x; A.normal[1] = Hit.Normal.y; A.normal[2] = Hit.Normal.z;
+                    A.u = Hit.UV.x; A.v = Hit.UV.y;
+                }
+            }
+        }
 }
 
 float oracle_fp_exp(float x) { return pt_exp(x); }

@@ -43,6 +43,12 @@ void oracle_trace_rays(const pt_scene_packs* packs, uint32_t n, const float* ori
  * out = OutColor (rgba32f), out8 = sRGB8 swapchain bytes (R,G,B,A). */
 void oracle_resolve(const float* accum, uint32_t n, const pt_resolve_parameters* params, float* out, uint8_t* out8);
 
+/* RenderPreview (preview_render.glsl:96-178) over RenderSizeX x RenderSizeY
+ * pixels: OutColor rgba (4 floats/px), primary-hit AOVs, and the pick query
+ * result (HitShapeIndex at MouseX, MouseY; untouched if outside). */
+void oracle_preview(const pt_scene_packs* packs, const pt_preview_parameters* params, float* rgba, pt_preview_aov* aov,
+                    uint32_t* hit_shape_index);
+
 /* Convention kernels, exposed for known-answer tests. */
 float oracle_fp_exp(float x);
 float oracle_fp_log(float x);

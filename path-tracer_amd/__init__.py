@@ -12,7 +12,11 @@ from .scene import (Scene, spectrum_coefficients, build_spectrum_table, load_spe
                     TEXTURE_RADIANCE, SCENE_DIRTY_ALL, RENDER_FLAG_ACCUMULATE, RENDER_FLAG_SAMPLE_JITTER)
 from .integrator import (Device, DeviceScene, SampleBuffer, BasicRenderer, Comm, PathTracerError, ResolveParameters,
                          device_count, CreateSampleBuffer, CreateBasicRenderer, ResetBasicRenderer, RunBasicRenderer,
-                         DestroyBasicRenderer, DestroySampleBuffer, RenderSampleBuffer)
+                         DestroyBasicRenderer, DestroySampleBuffer, RenderSampleBuffer, PreviewParameters,
+                         PreviewRenderContext, CreatePreviewRenderContext, RenderPreview, RetrievePreviewQueryResult)
+from ._native import (PREVIEW_RENDER_MODE_BASE_COLOR, PREVIEW_RENDER_MODE_BASE_COLOR_SHADED, PREVIEW_RENDER_MODE_NORMAL,
+                      PREVIEW_RENDER_MODE_MATERIAL_INDEX, PREVIEW_RENDER_MODE_PRIMITIVE_INDEX,
+                      PREVIEW_RENDER_MODE_MESH_COMPLEXITY, PREVIEW_RENDER_MODE_SCENE_COMPLEXITY)
 from ._native import TONE_MAPPING_CLAMP, TONE_MAPPING_REINHARD, TONE_MAPPING_HABLE, TONE_MAPPING_ACES
 from .image import write_png, write_ppm, write_pfm, read_png
 from .layout import band_rows, owned_pixels

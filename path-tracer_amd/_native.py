@@ -58,6 +58,22 @@ class pt_resolve_parameters(C.Structure):
     ]
 
 
+class pt_packed_transform(C.Structure):
+    _fields_ = [("To", C.c_float * 16), ("From", C.c_float * 16)]
+
+
+class pt_preview_parameters(C.Structure):
+    """preview_parameters (src/application/preview_render.hpp:22-33)."""
+    _fields_ = [
+        ("CameraTransform", pt_packed_transform),
+        ("RenderMode", C.c_uint32),
+        ("Brightness", C.c_float),
+        ("SelectedShapeIndex", C.c_uint32),
+        ("RenderSizeX", C.c_uint32), ("RenderSizeY", C.c_uint32),
+        ("MouseX", C.c_uint32), ("MouseY", C.c_uint32),
+    ]
+
+
 class pts_config_info(C.Structure):
     _fields_ = [
         ("width", C.c_uint32), ("height", C.c_uint32), ("spp", C.c_uint32), ("camera_count", C.c_uint32),
@@ -79,6 +95,13 @@ PIXEL_STATE_DTYPE = np.dtype([
     ("sample", "<f4", (3,)), ("active01", "<u4"), ("active23", "<u4"),
 ])
 assert PIXEL_STATE_DTYPE.itemsize == 96
+
+PREVIEW_AOV_DTYPE = np.dtype([
+    ("time", "<f4"), ("shape_index", "<u4"), ("material_index", "<u4"), ("primitive_index", "<u4"),
+    ("mesh_complexity", "<u4"), ("scene_complexity", "<u4"), ("normal", "<f4", (3,)), ("u", "<f4"), ("v", "<f4"),
+    ("reserved", "<u4"),
+])
+assert PREVIEW_AOV_DTYPE.itemsize == 48
 
 # Packed scene layouts (include/pt_packed.h) as numpy dtypes, for tests.
 SHAPE_NODE_DTYPE = np.dtype([("Minimum", "<f4", (3,)), ("ChildNodeIndices", "<u4"),
@@ -107,6 +130,10 @@ assert TEXTURE_DTYPE.itemsize == 32
 
 KERNEL_RAYGEN, KERNEL_EXTEND, KERNEL_SHADE, KERNEL_RESOLVE = 0, 1, 2, 3
 TONE_MAPPING_CLAMP, TONE_MAPPING_REINHARD, TONE_MAPPING_HABLE, TONE_MAPPING_ACES = 0, 1, 2, 3
+(PREVIEW_RENDER_MODE_BASE_COLOR, PREVIEW_RENDER_MODE_BASE_COLOR_SHADED, PREVIEW_RENDER_MODE_NORMAL,
+ PREVIEW_RENDER_MODE_MATERIAL_INDEX, PREVIEW_RENDER_MODE_PRIMITIVE_INDEX, PREVIEW_RENDER_MODE_MESH_COMPLEXITY,
+ PREVIEW_RENDER_MODE_SCENE_COMPLEXITY) = range(7)
+KERNEL_PREVIEW = 4
 
 _vp = C.c_void_p
 _u32 = C.c_uint32
@@ -178,6 +205,12 @@ HIP_API = {
     "ptBasicRendererSlotCount": (_u32, [_vp]),
     "ptReadBasicRendererState": (_i32, [_vp, _vp, _vp]),
     "ptTraceRays": (_i32, [_vp, _vp, _u32, _fptr, _u32ptr, _fptr, _vp]),
+    "ptCreatePreviewRenderContext": (_vp, [_vp, _vp]),
+    "ptDestroyPreviewRenderContext": (None, [_vp, _vp]),
+    "ptRenderPreview": (_i32, [_vp, _vp, C.POINTER(pt_preview_parameters)]),
+    "ptRetrievePreviewQueryResult": (_i32, [_vp, _vp, C.POINTER(C.c_uint32)]),
+    "ptReadPreviewImage": (_i32, [_vp, _vp, _fptr]),
+    "ptReadPreviewAOVs": (_i32, [_vp, _vp, _vp]),
     "ptCheckFastDivision": (_i32, [_vp, C.c_uint64, _u32, C.POINTER(C.c_uint64)]),
     "ptExtendStats": (_i32, [_vp, _vp, C.POINTER(C.c_uint64)]),
     "ptSetProfiling": (_i32, [_vp, _i32]),

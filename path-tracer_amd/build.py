@@ -20,7 +20,8 @@ INCLUDE = ROOT / "include"
 
 SCENE_SRC = sorted((CSRC / "scene").glob("*.cpp"))
 SCENE_HDR = sorted((CSRC / "scene").glob("*.hpp")) + sorted(INCLUDE.glob("*.h"))
-HIP_SRC = [CSRC / "hip" / "kernels.hip", CSRC / "hip" / "resolve.hip", CSRC / "hip" / "runtime.hip"]
+HIP_SRC = [CSRC / "hip" / "kernels.hip", CSRC / "hip" / "resolve.hip", CSRC / "hip" / "preview.hip",
+           CSRC / "hip" / "runtime.hip"]
 HIP_HDR = sorted((CSRC / "hip").glob("*.hpp")) + sorted(INCLUDE.glob("*.h"))
 
 SCENE_LIB = PKG / "libptscene.so"

@@ -14,346 +14,10 @@
 // t = s/256, so a 64-lane wave holds a 16x4 pixel block (coherent primary
 // rays) and a renderer can own an arbitrary set of 16-row bands.
 #include "pt_device.hpp"
+#include "traverse.hpp"
 #include "kernels.hpp"
 
 namespace ptd {
-
-// --- traversal stack: LDS columns + global spill ----------------------------
-
-template <bool SPILL, int CAP>
-struct tstack {
-    uint32_t* lds;        // &smem[tid]; entry i at lds[i * 256]
-    uint32_t* spill;      // &spill[thread]; entry i (>= CAP) at spill[(i - CAP) * stride]
-    uint32_t stride;
-    PT_DEV void put(uint32_t i, uint32_t v)
-    {
-        if (!SPILL || i < CAP) lds[i * 256] = v;
-        else spill[(i - CAP) * stride] = v;
-    }
-    PT_DEV uint32_t get(uint32_t i) const
-    {
-        if (!SPILL || i < CAP) return lds[i * 256];
-        return spill[(i - CAP) * stride];
-    }
-};
-
-// --- traversal ------------------------------------------------------------------
-//
-// Trace() (scene.glsl.inc:468-611) as a resumable state machine: every loop
-// iteration advances each active lane by ONE node of its own traversal, in
-// exactly the reference's order (near-first children, LIFO Stack[32] per
-// level, IntersectShape at TLAS leaves, IntersectMeshNode for mesh instances),
-// so every ray reaches the same closest hit bit for bit.  One flat loop over
-// both levels keeps a single loop-carried state (no nested divergent loops).
-
-struct lane_state {
-    pt3 O, V, Y;         // current-level ray (world at TLAS level, object space
-                         // inside a mesh) and its reciprocal velocity
-    float Time;          // Hit.Time
-    uint32_t Shape;      // Hit.ShapeIndex (0xFFFFFFFE = face of the current mesh)
-    uint32_t Prim;       // Hit.PrimitiveIndex
-    pt3 C;               // Hit.PrimitiveCoordinates
-    uint32_t na, nb;     // node being processed: TLAS {ChildNodeIndices, ShapeIndex},
-                         // BLAS {FaceBeginOrNodeIndex, FaceEndIndex}
-    uint32_t dT, dB;     // TLAS / BLAS stack depths (<= 32 each)
-    uint32_t blas;       // shape index of the mesh being traversed, NONE at TLAS level
-    bool exact;          // fast exact slab division applies to the current-level ray
-};
-
-PT_DEV void SetLevelRay(const dscene& S, lane_state& L, pt3 O, pt3 V)
-{
-    L.O = O;
-    L.V = V;
-    L.exact = S.fast_div && FastDivRay(O, V);
-    L.Y = v3(1.0f / V.x, 1.0f / V.y, 1.0f / V.z);
-}
-
-PT_DEV void LaneBegin(const dscene& S, lane_state& L, pt3 O, pt3 V, float Duration)
-{
-    SetLevelRay(S, L, O, V);
-    L.Time = Duration;
-    L.Shape = SHAPE_INDEX_NONE;
-    L.Prim = 0;
-    L.C = v3s(0);
-    L.dT = 0;
-    L.dB = 0;
-    L.blas = SHAPE_INDEX_NONE;
-    L.na = __float_as_uint(S.shape_nodes[0].w);
-    L.nb = __float_as_uint(S.shape_nodes[1].w);
-}
-
-// IntersectShape for the analytic shapes (scene.glsl.inc:413-465).
-PT_DEV void IntersectAnalytic(int32_t Type, pt3 O, pt3 V, uint32_t ShapeIndex, lane_state& L)
-{
-    if (Type == PT_SHAPE_TYPE_PLANE) {
-        float T = -O.z / V.z;
-        if (T < 0 || T > L.Time) return;
-        L.Time = T;
-        L.Shape = ShapeIndex;
-        L.Prim = 0;
-        L.C = O + V * T;
-    } else if (Type == PT_SHAPE_TYPE_SPHERE) {
-        float Vv = dot(V, V);
-        float P = dot(O, V);
-        float Q = dot(O, O) - 1.0f;
-        float D2 = P * P - Q * Vv;
-        if (D2 < 0) return;
-        float D = pt_sqrt(D2);
-        if (D < P) return;
-        float S0 = -P - D;
-        float S1 = -P + D;
-        float Sv = S0 < 0 ? S1 : S0;
-        if (Sv < 0 || Sv > Vv * L.Time) return;
-        L.Time = Sv / Vv;
-        L.Shape = ShapeIndex;
-        L.Prim = 0;
-        L.C = O + V * L.Time;
-    } else if (Type == PT_SHAPE_TYPE_CUBE) {
-        pt3 Mn = (v3s(-1) - O) / V;
-        pt3 Mx = (v3s(+1) - O) / V;
-        pt3 E = vmin(Mn, Mx);
-        pt3 Lt = vmax(Mn, Mx);
-        float T0 = pt_max(pt_max(E.x, E.y), E.z);
-        float T1 = pt_min(pt_min(Lt.x, Lt.y), Lt.z);
-        if (T1 < T0) return;
-        if (T1 <= 0) return;
-        float T = T0 < 0 ? T1 : T0;
-        if (T >= L.Time) return;
-        L.Time = T;
-        L.Shape = ShapeIndex;
-        L.Prim = 0;
-        L.C = O + V * T;
-    }
-}
-
-// IntersectMeshFace (scene.glsl.inc:304-334) on the lane's object-space ray.
-PT_DEV void LaneMeshFace(const dscene& S, uint32_t F, lane_state& L)
-{
-    float4 a = S.mesh_faces[3 * F + 0], b = S.mesh_faces[3 * F + 1], c = S.mesh_faces[3 * F + 2];
-    pt3 P0 = xyz(a);
-    pt3 Edge1 = xyz(b) - P0;
-    pt3 Edge2 = xyz(c) - P0;
-    pt3 RCE2 = cross(L.V, Edge2);
-    float Det = dot(Edge1, RCE2);
-    if (pt_abs(Det) < PT_EPSILON) return;
-    float InvDet = 1.0f / Det;
-    pt3 Sv = L.O - P0;
-    float U = InvDet * dot(Sv, RCE2);
-    if (U < 0 || U > 1) return;
-    pt3 SCE1 = cross(Sv, Edge1);
-    float W = InvDet * dot(L.V, SCE1);
-    if (W < 0 || U + W > 1) return;
-    float T = InvDet * dot(Edge2, SCE1);
-    if (T < 0 || T > L.Time) return;
-    L.Time = T;
-    L.Shape = 0xFFFFFFFEu;
-    L.Prim = F;
-    L.C = v3(1 - U - W, U, W);
-}
-
-// Traversal statistics hooks: no-ops in the render kernel, counters in the
-// diagnostic instantiation (ptExtendStats).
-struct no_stats {
-    PT_DEV void step() {}
-    PT_DEV void internal() {}
-    PT_DEV void leaf(uint32_t) {}
-    PT_DEV void shape() {}
-    PT_DEV void pop() {}
-};
-struct lane_stats {
-    uint32_t steps = 0, internals = 0, leaves = 0, faces = 0, shapes = 0, pops = 0;
-    PT_DEV void step() { steps++; }
-    PT_DEV void internal() { internals++; }
-    PT_DEV void leaf(uint32_t n) { leaves++; faces += n; }
-    PT_DEV void shape() { shapes++; }
-    PT_DEV void pop() { pops++; }
-};
-
-// BLAS stack entries.  When the scene allows (dscene::blas_words, checked on
-// the host) an entry is the pushed node's own index words, packed: leaf ->
-// 1<<31 | count<<26 | first face (count <= 31, first face < 2^26); internal ->
-// child-pair index (< 2^31).  A pop is then an LDS read only.  Otherwise the
-// entry is the node index and a pop reloads its words (two global loads).
-PT_DEV uint32_t PackBlasEntry(uint32_t w0, uint32_t w1)
-{
-    return w1 > 0 ? (0x80000000u | ((w1 - w0) << 26) | w0) : w0;
-}
-
-PT_DEV void UnpackBlasEntry(uint32_t e, uint32_t& na, uint32_t& nb)
-{
-    if (e >> 31) {
-        na = e & 0x03FFFFFFu;
-        nb = na + ((e >> 26) & 31u);
-    } else {
-        na = e;
-        nb = 0;
-    }
-}
-
-// Advances one lane by one node.  Returns true when its Trace() is complete.
-// Only the two index words of the current node are carried between steps;
-// its bounds were already consumed by the parent's box test.
-template <bool SPILL, int CAP, class Src, class Stats = no_stats>
-PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, const Src& src, uint32_t slot,
-                     Stats& ss)
-{
-    ss.step();
-    const uint32_t* mesh_words = reinterpret_cast<const uint32_t*>(S.mesh_nodes);
-    const uint32_t* shape_words = reinterpret_cast<const uint32_t*>(S.shape_nodes);
-    if (L.blas != SHAPE_INDEX_NONE) {
-        // IntersectMeshNode (scene.glsl.inc:336-399), one node.
-        if (L.nb > 0) {
-            ss.leaf(L.nb - L.na);
-            for (uint32_t F = L.na; F < L.nb; F++) LaneMeshFace(S, F, L);
-        } else {
-            ss.internal();
-            uint32_t Index = L.na;
-            float4 a0 = S.mesh_nodes[2 * Index], a1 = S.mesh_nodes[2 * Index + 1];
-            float4 b0 = S.mesh_nodes[2 * Index + 2], b1 = S.mesh_nodes[2 * Index + 3];
-            float TA = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, a0, a1, L.exact);
-            float TB = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, b0, b1, L.exact);
-            if (TA > TB) {
-                if (TA < PT_INFINITY && L.dB < 32)
-                    st.put(L.dT + L.dB++, S.blas_words ? PackBlasEntry(__float_as_uint(a0.w), __float_as_uint(a1.w))
-                                                       : Index);
-                L.na = __float_as_uint(b0.w); L.nb = __float_as_uint(b1.w);
-                return false;
-            }
-            if (TB < PT_INFINITY) {
-                if (L.dB < 32)
-                    st.put(L.dT + L.dB++, S.blas_words ? PackBlasEntry(__float_as_uint(b0.w), __float_as_uint(b1.w))
-                                                       : Index + 1);
-                L.na = __float_as_uint(a0.w); L.nb = __float_as_uint(a1.w);
-                return false;
-            }
-            if (TA < PT_INFINITY) { L.na = __float_as_uint(a0.w); L.nb = __float_as_uint(a1.w); return false; }
-        }
-        if (L.dB > 0) {
-            ss.pop();
-            uint32_t E = st.get(L.dT + --L.dB);
-            if (S.blas_words) {
-                UnpackBlasEntry(E, L.na, L.nb);
-            } else {
-                L.na = mesh_words[8 * E + 3];
-                L.nb = mesh_words[8 * E + 7];
-            }
-            return false;
-        }
-        // IntersectMeshNode returned (scene.glsl.inc:409-411); back to the
-        // world-space ray for the rest of the shape traversal.
-        if (L.Shape == 0xFFFFFFFEu) L.Shape = L.blas;
-        L.blas = SHAPE_INDEX_NONE;
-        if (L.dT == 0) return true;
-        pt3 WO, WV;
-        float D;
-        src.load(slot, WO, WV, D);
-        SetLevelRay(S, L, WO, WV);
-    } else {
-        // Intersect (scene.glsl.inc:468-520), one node.
-        uint32_t Children = L.na;
-        if (Children == 0) {
-            ss.shape();
-            uint32_t ShapeIndex = L.nb;
-            const pt_packed_shape* Shape = &S.shapes[ShapeIndex];
-            const float* From = Shape->Transform.From;
-            pt3 O = mat4_mul_point(From, L.O);
-            pt3 V = mat4_mul_vector(From, L.V);
-            int32_t Type = Shape->Type;
-            if (Type == PT_SHAPE_TYPE_MESH_INSTANCE) {
-                uint32_t Root = Shape->MeshRootNodeIndex;
-                SetLevelRay(S, L, O, V);
-                L.blas = ShapeIndex;
-                L.dB = 0;
-                L.na = mesh_words[8 * Root + 3];
-                L.nb = mesh_words[8 * Root + 7];
-                return false;
-            }
-            IntersectAnalytic(Type, O, V, ShapeIndex, L);
-        } else {
-            ss.internal();
-            uint32_t IA = Children & 0xFFFF, IB = Children >> 16;
-            float4 a0 = S.shape_nodes[2 * IA], a1 = S.shape_nodes[2 * IA + 1];
-            float4 b0 = S.shape_nodes[2 * IB], b1 = S.shape_nodes[2 * IB + 1];
-            float TA = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, a0, a1, L.exact);
-            float TB = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, b0, b1, L.exact);
-            if (TA > TB) {
-                if (TA < PT_INFINITY && L.dT < 32) st.put(L.dT++, IA);
-                L.na = __float_as_uint(b0.w); L.nb = __float_as_uint(b1.w);
-                return false;
-            }
-            if (TB < PT_INFINITY) {
-                if (L.dT < 32) st.put(L.dT++, IB);
-                L.na = __float_as_uint(a0.w); L.nb = __float_as_uint(a1.w);
-                return false;
-            }
-            if (TA < PT_INFINITY) { L.na = __float_as_uint(a0.w); L.nb = __float_as_uint(a1.w); return false; }
-        }
-    }
-    if (L.dT > 0) {
-        ss.pop();
-        uint32_t I = st.get(--L.dT);
-        L.na = shape_words[8 * I + 3];
-        L.nb = shape_words[8 * I + 7];
-        return false;
-    }
-    return true;
-}
-
-// Hit attribute reconstruction (scene.glsl.inc:535-608).
-PT_DEV void HitAttributes(const dscene& S, uint32_t ShapeIndex, uint32_t Prim, pt3 C, uint32_t& Material, pt3& Normal,
-                          pt3& TangentX, pt2& UV)
-{
-    const pt_packed_shape* Shape = &S.shapes[ShapeIndex];
-    Material = Shape->MaterialIndex;
-    int32_t Type = Shape->Type;
-    const float* To = Shape->Transform.To;
-    const float* From = Shape->Transform.From;
-    if (Type == PT_SHAPE_TYPE_MESH_INSTANCE) {
-        float4 f0 = S.mesh_faces[3 * Prim + 0];
-        float4 f1 = S.mesh_faces[3 * Prim + 1];
-        float4 f2 = S.mesh_faces[3 * Prim + 2];
-        uint2 V0 = S.mesh_vertices[__float_as_uint(f0.w)];
-        uint2 V1 = S.mesh_vertices[__float_as_uint(f1.w)];
-        uint2 V2 = S.mesh_vertices[__float_as_uint(f2.w)];
-        pt3 N = SafeNormalize(UnpackUnitVector(V0.x) * C.x + UnpackUnitVector(V1.x) * C.y + UnpackUnitVector(V2.x) * C.z);
-        Normal = TransformNormal(N, From);
-        TangentX = ComputeTangentVector(Normal);
-        pt2 UV0 = v2(pt_half_to_float(V0.y & 0xFFFF), pt_half_to_float(V0.y >> 16));
-        pt2 UV1 = v2(pt_half_to_float(V1.y & 0xFFFF), pt_half_to_float(V1.y >> 16));
-        pt2 UV2 = v2(pt_half_to_float(V2.y & 0xFFFF), pt_half_to_float(V2.y >> 16));
-        UV = UV0 * C.x + UV1 * C.y + UV2 * C.z;
-    } else if (Type == PT_SHAPE_TYPE_PLANE) {
-        Normal = TransformNormal(v3(0, 0, 1), From);
-        TangentX = TransformDirection(v3(1, 0, 0), To);
-        UV = v2(pt_fract(C.x), pt_fract(C.y));
-    } else if (Type == PT_SHAPE_TYPE_SPHERE) {
-        pt3 P = C;
-        float U = (pt_atan2(P.y, P.x) + PT_PI) / PT_TAU;
-        float W = (P.z + 1.0f) / 2.0f;
-        Normal = TransformNormal(P, From);
-        TangentX = TransformDirection(cross(P, v3(-P.y, P.x, 0)), To);
-        UV = v2(U, W);
-    } else {
-        pt3 P = C;
-        pt3 Q = vabs(P);
-        pt3 N, T;
-        if (Q.x >= Q.y && Q.x >= Q.z) {
-            float Sg = pt_sign(P.x);
-            N = v3(Sg, 0, 0); T = v3(0, Sg, 0);
-            UV = 0.5f * v2(1.0f + P.y, 1.0f + P.z);
-        } else if (Q.y >= Q.x && Q.y >= Q.z) {
-            float Sg = pt_sign(P.y);
-            N = v3(0, Sg, 0); T = v3(0, 0, Sg);
-            UV = 0.5f * v2(1.0f + P.x, 1.0f + P.z);
-        } else {
-            float Sg = pt_sign(P.z);
-            N = v3(0, 0, Sg); T = v3(Sg, 0, 0);
-            UV = 0.5f * v2(1.0f + P.x, 1.0f + P.y);
-        }
-        Normal = TransformNormal(N, From);
-        TangentX = TransformDirection(T, To);
-    }
-}
 
 // --- slot / pixel mapping ---------------------------------------------------
 

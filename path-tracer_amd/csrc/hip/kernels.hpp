@@ -61,6 +61,9 @@ enum : uint32_t {
     PT_MATS_ALL = 15,
 };
 uint32_t pt_shade_mats(uint32_t scene_mats);
+hipError_t pt_launch_preview(const ptd::dscene& S, const pt_preview_parameters* p, uint32_t* spill, float4* out,
+                             pt_preview_aov* aov, uint32_t* query, hipStream_t st);
+uint32_t pt_preview_stack_cap();
 hipError_t pt_launch_resolve(const float4* accum, uint32_t n, float brightness, uint32_t mode, float white, float4* out,
                              uint32_t* out8, hipStream_t st);
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,

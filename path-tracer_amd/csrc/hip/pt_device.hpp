@@ -422,18 +422,21 @@ PT_DEV pt4 SampleTexture(const dscene& S, uint32_t Index, pt2 UV)
     return ((1 - A) * (1 - B)) * T00 + (A * (1 - B)) * T10 + ((1 - A) * B) * T01 + (A * B) * T11;
 }
 
+// SampleSkyboxSpectrum (scene.glsl.inc:209-221)
+PT_DEV pt4 SampleSkyboxSpectrum(const dscene& S, pt3 D)
+{
+    if (S.g.SkyboxTextureIndex == TEXTURE_INDEX_NONE) return v4(0, 0, 100, 1);
+    float Phi = pt_atan2(D.y, D.x);
+    float Theta = pt_asin(D.z);
+    float U = 0.5f + Phi / PT_TAU;
+    float V = 0.5f + Theta / PT_PI;
+    return SampleTexture(S, S.g.SkyboxTextureIndex, v2(U, V));
+}
+
+// SampleSkyboxRadiance (scene.glsl.inc:225-229)
 PT_DEV pt4 SampleSkyboxRadiance(const dscene& S, pt3 D, pt4 Lambda)
 {
-    pt4 Spectrum;
-    if (S.g.SkyboxTextureIndex == TEXTURE_INDEX_NONE) {
-        Spectrum = v4(0, 0, 100, 1);
-    } else {
-        float Phi = pt_atan2(D.y, D.x);
-        float Theta = pt_asin(D.z);
-        float U = 0.5f + Phi / PT_TAU;
-        float V = 0.5f + Theta / PT_PI;
-        Spectrum = SampleTexture(S, S.g.SkyboxTextureIndex, v2(U, V));
-    }
+    pt4 Spectrum = SampleSkyboxSpectrum(S, D);
     return (Spectrum.w * SampleParametricSpectrum(v3(Spectrum.x, Spectrum.y, Spectrum.z), Lambda)) * S.g.SkyboxBrightness;
 }
 

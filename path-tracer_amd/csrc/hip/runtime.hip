@@ -113,6 +113,17 @@ struct pt_sample_buffer {
     bool resolved = false;
 };
 
+struct pt_preview {
+    pt_device* dev = nullptr;
+    pt_scene* scene = nullptr;           // non-owning (preview_render.hpp:20)
+    uint32_t width = 0, height = 0;
+    dbuf<float4> image;
+    dbuf<pt_preview_aov> aov;
+    dbuf<uint32_t> spill;
+    uint32_t* query = nullptr;
+    bool rendered = false;
+};
+
 struct pt_basic_renderer {
     pt_basic_renderer_params params{};
     pt_device* dev = nullptr;
@@ -729,6 +740,98 @@ int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state*
         O.active01 = act[s].x;
         O.active23 = act[s].y;
     }
+    return 0;
+}
+
+pt_preview* ptCreatePreviewRenderContext(pt_device* d, pt_scene* s)
+{
+    if (!d || !s) { SetError("null argument"); return nullptr; }
+    if (hipSetDevice(d->id) != hipSuccess) { SetError("hipSetDevice failed"); return nullptr; }
+    pt_preview* c = new pt_preview;
+    c->dev = d;
+    c->scene = s;
+    uint32_t none = 0xFFFFFFFFu;
+    if (hipMalloc(&c->query, sizeof(uint32_t)) != hipSuccess ||
+        hipMemcpy(c->query, &none, sizeof(none), hipMemcpyHostToDevice) != hipSuccess) {
+        SetError("preview query buffer allocation failed");
+        if (c->query) (void)hipFree(c->query);
+        delete c;
+        return nullptr;
+    }
+    return c;
+}
+
+void ptDestroyPreviewRenderContext(pt_device* d, pt_preview* c)
+{
+    if (!c) return;
+    if (d) (void)hipSetDevice(d->id);
+    c->image.release();
+    c->aov.release();
+    c->spill.release();
+    if (c->query) (void)hipFree(c->query);
+    delete c;
+}
+
+// RenderPreview (preview_render.cpp:118-181)
+int ptRenderPreview(pt_device* d, pt_preview* c, const pt_preview_parameters* p)
+{
+    if (!d || !c || !p) { SetError("null argument"); return -1; }
+    if (!c->scene->valid) { SetError("preview: scene has no valid packs (call ptUpdateScene)"); return -1; }
+    if (p->RenderMode > PT_PREVIEW_RENDER_MODE_SCENE_COMPLEXITY) { SetError("bad preview mode %u", p->RenderMode); return -1; }
+    if (p->RenderSizeX == 0 || p->RenderSizeY == 0 || p->RenderSizeX > 32768 || p->RenderSizeY > 32768) {
+        SetError("bad preview size %ux%u", p->RenderSizeX, p->RenderSizeY);
+        return -1;
+    }
+    PT_HIP(hipSetDevice(d->id));
+    size_t n = (size_t)p->RenderSizeX * p->RenderSizeY;
+    PT_HIP(c->image.alloc(n));
+    PT_HIP(c->aov.alloc(n));
+    uint32_t need = c->scene->stack_needed, cap = pt_preview_stack_cap();
+    uint32_t* spill = nullptr;
+    if (need > cap) {
+        size_t threads = (size_t)((p->RenderSizeX + 15) / 16) * ((p->RenderSizeY + 15) / 16) * 256;
+        PT_HIP(c->spill.alloc((need - cap) * threads));
+        spill = c->spill.ptr;
+    }
+    event_pair ep{};
+    if (int e = BeginTimed(d, PT_KERNEL_PREVIEW, ep)) return e;
+    PT_HIP(pt_launch_preview(c->scene->d, p, spill, c->image.ptr, c->aov.ptr, c->query, d->stream));
+    if (int e = EndTimed(d, ep)) return e;
+    c->width = p->RenderSizeX;
+    c->height = p->RenderSizeY;
+    c->rendered = true;
+    return 0;
+}
+
+// RetrievePreviewQueryResult (preview_render.cpp:96-116)
+int ptRetrievePreviewQueryResult(pt_device* d, pt_preview* c, uint32_t* hit_shape_index)
+{
+    if (!d || !c || !hit_shape_index) { SetError("null argument"); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    PT_HIP(hipMemcpyAsync(hit_shape_index, c->query, sizeof(uint32_t), hipMemcpyDeviceToHost, d->stream));
+    PT_HIP(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+int ptReadPreviewImage(pt_device* d, pt_preview* c, float* rgba)
+{
+    if (!d || !c || !rgba) { SetError("null argument"); return -1; }
+    if (!c->rendered) { SetError("preview not rendered"); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    PT_HIP(hipMemcpyAsync(rgba, c->image.ptr, (size_t)c->width * c->height * sizeof(float4), hipMemcpyDeviceToHost,
+                          d->stream));
+    PT_HIP(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+int ptReadPreviewAOVs(pt_device* d, pt_preview* c, pt_preview_aov* aov)
+{
+    if (!d || !c || !aov) { SetError("null argument"); return -1; }
+    if (!c->rendered) { SetError("preview not rendered"); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    PT_HIP(hipMemcpyAsync(aov, c->aov.ptr, (size_t)c->width * c->height * sizeof(pt_preview_aov),
+                          hipMemcpyDeviceToHost, d->stream));
+    PT_HIP(hipStreamSynchronize(d->stream));
     return 0;
 }
 

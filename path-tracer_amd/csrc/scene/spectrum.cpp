@@ -4,6 +4,7 @@
 // the Beta-independent factor Observer(λ)·D65(λ) of each of the 471 samples
 // is computed once (same operands, same order, so the same bits).
 #include "spectrum.hpp"
+#include "../../../include/pt_cie.h"
 
 #include <cstdio>
 #include <cstdlib>
@@ -35,56 +36,7 @@ vec3 MulMat3(const float* m, vec3 v)
 }
 
 // spectrum.cpp:33-129 (CIE D65, 360..830 nm, 1 nm steps)
-const float D65[471] = {
-     46.638f,  47.183f,  47.728f,  48.273f,  48.819f,  49.364f,  49.909f,  50.454f,  50.999f,  51.544f,
-     52.089f,  51.878f,  51.666f,  51.455f,  51.244f,  51.032f,  50.821f,  50.610f,  50.398f,  50.187f,
-     49.975f,  50.443f,  50.910f,  51.377f,  51.845f,  52.312f,  52.779f,  53.246f,  53.714f,  54.181f,
-     54.648f,  57.459f,  60.270f,  63.080f,  65.891f,  68.701f,  71.512f,  74.323f,  77.134f,  79.944f,
-     82.755f,  83.628f,  84.501f,  85.374f,  86.247f,  87.120f,  87.994f,  88.867f,  89.740f,  90.613f,
-     91.486f,  91.681f,  91.875f,  92.070f,  92.264f,  92.459f,  92.653f,  92.848f,  93.043f,  93.237f,
-     93.432f,  92.757f,  92.082f,  91.407f,  90.732f,  90.057f,  89.382f,  88.707f,  88.032f,  87.357f,
-     86.682f,  88.501f,  90.319f,  92.137f,  93.955f,  95.774f,  97.592f,  99.410f, 101.228f, 103.047f,
-    104.865f, 106.079f, 107.294f, 108.508f, 109.722f, 110.936f, 112.151f, 113.365f, 114.579f, 115.794f,
-    117.008f, 117.088f, 117.169f, 117.249f, 117.330f, 117.410f, 117.490f, 117.571f, 117.651f, 117.732f,
-    117.812f, 117.517f, 117.222f, 116.927f, 116.632f, 116.336f, 116.041f, 115.746f, 115.451f, 115.156f,
-    114.861f, 114.967f, 115.073f, 115.180f, 115.286f, 115.392f, 115.498f, 115.604f, 115.711f, 115.817f,
-    115.923f, 115.212f, 114.501f, 113.789f, 113.078f, 112.367f, 111.656f, 110.945f, 110.233f, 109.522f,
-    108.811f, 108.865f, 108.920f, 108.974f, 109.028f, 109.082f, 109.137f, 109.191f, 109.245f, 109.300f,
-    109.354f, 109.199f, 109.044f, 108.888f, 108.733f, 108.578f, 108.423f, 108.268f, 108.112f, 107.957f,
-    107.802f, 107.501f, 107.200f, 106.898f, 106.597f, 106.296f, 105.995f, 105.694f, 105.392f, 105.091f,
-    104.790f, 105.080f, 105.370f, 105.660f, 105.950f, 106.239f, 106.529f, 106.819f, 107.109f, 107.399f,
-    107.689f, 107.361f, 107.032f, 106.704f, 106.375f, 106.047f, 105.719f, 105.390f, 105.062f, 104.733f,
-    104.405f, 104.369f, 104.333f, 104.297f, 104.261f, 104.225f, 104.190f, 104.154f, 104.118f, 104.082f,
-    104.046f, 103.641f, 103.237f, 102.832f, 102.428f, 102.023f, 101.618f, 101.214f, 100.809f, 100.405f,
-    100.000f,  99.633f,  99.267f,  98.900f,  98.534f,  98.167f,  97.800f,  97.434f,  97.067f,  96.701f,
-     96.334f,  96.280f,  96.225f,  96.170f,  96.116f,  96.061f,  96.007f,  95.952f,  95.897f,  95.843f,
-     95.788f,  95.078f,  94.368f,  93.657f,  92.947f,  92.237f,  91.527f,  90.816f,  90.106f,  89.396f,
-     88.686f,  88.818f,  88.950f,  89.082f,  89.214f,  89.346f,  89.478f,  89.610f,  89.742f,  89.874f,
-     90.006f,  89.966f,  89.925f,  89.884f,  89.843f,  89.803f,  89.762f,  89.721f,  89.680f,  89.640f,
-     89.599f,  89.409f,  89.219f,  89.029f,  88.839f,  88.649f,  88.459f,  88.269f,  88.079f,  87.889f,
-     87.699f,  87.258f,  86.817f,  86.376f,  85.935f,  85.494f,  85.053f,  84.612f,  84.171f,  83.730f,
-     83.289f,  83.330f,  83.371f,  83.412f,  83.453f,  83.494f,  83.535f,  83.576f,  83.617f,  83.658f,
-     83.699f,  83.332f,  82.965f,  82.597f,  82.230f,  81.863f,  81.496f,  81.129f,  80.761f,  80.394f,
-     80.027f,  80.046f,  80.064f,  80.083f,  80.102f,  80.121f,  80.139f,  80.158f,  80.177f,  80.196f,
-     80.215f,  80.421f,  80.627f,  80.834f,  81.040f,  81.246f,  81.453f,  81.659f,  81.865f,  82.072f,
-     82.278f,  81.878f,  81.479f,  81.080f,  80.680f,  80.281f,  79.882f,  79.482f,  79.083f,  78.684f,
-     78.284f,  77.428f,  76.572f,  75.715f,  74.859f,  74.003f,  73.147f,  72.290f,  71.434f,  70.578f,
-     69.721f,  69.910f,  70.099f,  70.288f,  70.476f,  70.665f,  70.854f,  71.043f,  71.231f,  71.420f,
-     71.609f,  71.883f,  72.157f,  72.431f,  72.705f,  72.979f,  73.253f,  73.527f,  73.801f,  74.075f,
-     74.349f,  73.075f,  71.800f,  70.525f,  69.251f,  67.977f,  66.702f,  65.427f,  64.153f,  62.879f,
-     61.604f,  62.432f,  63.260f,  64.088f,  64.917f,  65.745f,  66.573f,  67.401f,  68.229f,  69.057f,
-     69.886f,  70.406f,  70.926f,  71.446f,  71.966f,  72.486f,  73.006f,  73.527f,  74.047f,  74.567f,
-     75.087f,  73.938f,  72.788f,  71.639f,  70.489f,  69.340f,  68.190f,  67.041f,  65.892f,  64.742f,
-     63.593f,  61.875f,  60.158f,  58.440f,  56.723f,  55.005f,  53.288f,  51.571f,  49.853f,  48.136f,
-     46.418f,  48.457f,  50.496f,  52.534f,  54.573f,  56.612f,  58.651f,  60.689f,  62.728f,  64.767f,
-     66.805f,  66.463f,  66.121f,  65.779f,  65.436f,  65.094f,  64.752f,  64.410f,  64.067f,  63.725f,
-     63.383f,  63.475f,  63.567f,  63.659f,  63.751f,  63.843f,  63.935f,  64.028f,  64.120f,  64.212f,
-     64.304f,  63.819f,  63.334f,  62.848f,  62.363f,  61.878f,  61.393f,  60.907f,  60.422f,  59.937f,
-     59.452f,  58.703f,  57.953f,  57.204f,  56.455f,  55.705f,  54.956f,  54.207f,  53.458f,  52.708f,
-     51.959f,  52.507f,  53.055f,  53.603f,  54.152f,  54.700f,  55.248f,  55.796f,  56.344f,  56.892f,
-     57.441f,  57.728f,  58.015f,  58.302f,  58.589f,  58.877f,  59.164f,  59.451f,  59.738f,  60.025f,
-     60.312f,
-};
+const float D65[471] = {PT_CIE_D65_VALUES};
 
 struct dvec3 {
     double x = 0, y = 0, z = 0;

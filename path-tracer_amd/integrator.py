@@ -236,6 +236,65 @@ class BasicRenderer:
             self._h = None
 
 
+class PreviewParameters:
+    """preview_parameters (preview_render.hpp:22-33).  camera_to: the camera's
+    4x4 world transform (column-major 16 floats or a (4,4) array, like
+    packed_transform.To); From is not read by the preview."""
+
+    def __init__(self, camera_to, RenderMode=0, Brightness=1.0, SelectedShapeIndex=0xFFFFFFFF,
+                 RenderSizeX=640, RenderSizeY=360, MouseX=0xFFFFFFFF, MouseY=0xFFFFFFFF):
+        m = np.asarray(camera_to, dtype=np.float32)
+        self.camera_to = (m.T.reshape(-1) if m.shape == (4, 4) else m.reshape(-1)).copy()
+        self.RenderMode, self.Brightness, self.SelectedShapeIndex = int(RenderMode), float(Brightness), int(SelectedShapeIndex)
+        self.RenderSizeX, self.RenderSizeY, self.MouseX, self.MouseY = int(RenderSizeX), int(RenderSizeY), int(MouseX), int(MouseY)
+
+    def as_struct(self) -> N.pt_preview_parameters:
+        p = N.pt_preview_parameters()
+        p.CameraTransform.To[:] = [float(x) for x in self.camera_to]
+        p.RenderMode, p.Brightness, p.SelectedShapeIndex = self.RenderMode, self.Brightness, self.SelectedShapeIndex
+        p.RenderSizeX, p.RenderSizeY, p.MouseX, p.MouseY = self.RenderSizeX, self.RenderSizeY, self.MouseX, self.MouseY
+        return p
+
+
+class PreviewRenderContext:
+    """preview_render_context (preview_render.hpp:15-20): primary-ray preview,
+    AOVs and pick queries over a DeviceScene."""
+
+    def __init__(self, device: Device, scene: DeviceScene):
+        L = N.hip_lib()
+        self.device, self.scene = device, scene
+        self._h = L.ptCreatePreviewRenderContext(device.handle, scene.handle)
+        if not self._h:
+            raise PathTracerError(L.ptGetLastError().decode())
+        self._size = (0, 0)
+
+    def render(self, params: PreviewParameters):
+        _check(N.hip_lib().ptRenderPreview(self.device.handle, self._h, C.byref(params.as_struct())), "ptRenderPreview")
+        self._size = (params.RenderSizeY, params.RenderSizeX)
+
+    def query(self) -> int:
+        """RetrievePreviewQueryResult: shape index under the mouse (0xFFFFFFFF = none)."""
+        v = C.c_uint32(0)
+        _check(N.hip_lib().ptRetrievePreviewQueryResult(self.device.handle, self._h, C.byref(v)),
+               "ptRetrievePreviewQueryResult")
+        return int(v.value)
+
+    def image(self) -> np.ndarray:
+        out = np.zeros(self._size + (4,), dtype=np.float32)
+        _check(N.hip_lib().ptReadPreviewImage(self.device.handle, self._h, N.fptr(out)), "ptReadPreviewImage")
+        return out
+
+    def aovs(self) -> np.ndarray:
+        out = np.zeros(self._size, dtype=N.PREVIEW_AOV_DTYPE)
+        _check(N.hip_lib().ptReadPreviewAOVs(self.device.handle, self._h, out.ctypes.data), "ptReadPreviewAOVs")
+        return out
+
+    def close(self):
+        if self._h:
+            N.hip_lib().ptDestroyPreviewRenderContext(self.device.handle, self._h)
+            self._h = None
+
+
 class Comm:
     """RCCL communicator (one process per GPU) for the frame-end reduce."""
 
@@ -291,3 +350,15 @@ def DestroySampleBuffer(device: Device, sample_buffer: SampleBuffer):
 
 def RenderSampleBuffer(device: Device, sample_buffer: SampleBuffer, parameters: ResolveParameters):
     sample_buffer.render(parameters)
+
+
+def CreatePreviewRenderContext(device: Device, scene: DeviceScene) -> PreviewRenderContext:
+    return PreviewRenderContext(device, scene)
+
+
+def RenderPreview(device: Device, context: PreviewRenderContext, parameters: PreviewParameters):
+    context.render(parameters)
+
+
+def RetrievePreviewQueryResult(device: Device, context: PreviewRenderContext) -> int:
+    return context.query()

@@ -52,6 +52,7 @@ def lib():
         L.oracle_unpack_unit_vector.argtypes = [u32, fptr]
         L.oracle_sample_observer.argtypes = [f32, fptr]
         L.oracle_resolve.argtypes = [fptr, u32, vp, fptr, C.POINTER(C.c_uint8)]
+        L.oracle_preview.argtypes = [vp, vp, fptr, vp, C.POINTER(C.c_uint32)]
         _lib = L
     return _lib
 
@@ -149,3 +150,16 @@ def resolve(accum: np.ndarray, brightness=1.0, mode=0, white=1.0):
     lib().oracle_resolve(a.ctypes.data_as(C.POINTER(C.c_float)), n, C.addressof(p),
                          out.ctypes.data_as(C.POINTER(C.c_float)), out8.ctypes.data_as(C.POINTER(C.c_uint8)))
     return out, out8
+
+
+def preview(packs, params):
+    """RenderPreview restated on the CPU: (OutColor (H,W,4), AOVs (H,W), query)."""
+    from path_tracer_amd import _native as N
+    p = params.as_struct()
+    H, W = params.RenderSizeY, params.RenderSizeX
+    img = np.zeros((H, W, 4), dtype=np.float32)
+    aov = np.zeros((H, W), dtype=N.PREVIEW_AOV_DTYPE)
+    q = C.c_uint32(0xFFFFFFFF)
+    lib().oracle_preview(C.addressof(packs), C.addressof(p), img.ctypes.data_as(C.POINTER(C.c_float)),
+                         aov.ctypes.data, C.byref(q))
+    return img, aov, int(q.value)

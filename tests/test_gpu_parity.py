@@ -281,3 +281,25 @@ def test_resolve_bit_exact(pt, dev, mode):
     assert same.all(), np.argwhere(~same)[:5]
     assert np.array_equal(out8, ref8)
     sb.close()
+
+
+@pytest.mark.parametrize("config", [1, 3, 5])
+@pytest.mark.parametrize("mode", range(7))
+def test_preview_bit_exact(pt, dev, config, mode):
+    """RenderPreview on the device vs the oracle: image, AOVs, pick query."""
+    s = scene_for(pt, config)
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    cam = s.arrays()["cameras"][0]["Transform"]["To"]
+    p = pt.PreviewParameters(cam, RenderMode=mode, RenderSizeX=72, RenderSizeY=40, Brightness=1.5,
+                             SelectedShapeIndex=1, MouseX=30, MouseY=21)
+    ctx = pt.PreviewRenderContext(dev, ds)
+    ctx.render(p)
+    img, aov, q = ctx.image(), ctx.aovs(), ctx.query()
+    ref_img, ref_aov, ref_q = oracle_lib.preview(s.packs(), p)
+    same = (img.view(np.uint32) == ref_img.view(np.uint32)) | (np.isnan(img) & np.isnan(ref_img))
+    assert same.all(), np.argwhere(~same)[:5]
+    assert np.array_equal(aov.view(np.uint8), ref_aov.view(np.uint8))
+    assert q == ref_q
+    ctx.close()
+    ds.close()
