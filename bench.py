@@ -179,9 +179,17 @@ def main():
     else:
         total_slots = float(slots_owned)
 
-    if rank != 0:
+    def shutdown():
+        for x in (r, sb, dscene):
+            x.close()
+        if comm is not None:
+            comm.close()
+        dev.close()
         if dist is not None:
             dist.destroy_process_group()
+
+    if rank != 0:
+        shutdown()
         return
 
     rays = total_slots * args.steps
@@ -248,15 +256,10 @@ def main():
         "cache_gbps": round(cache_bytes * slots_owned / (avg_ext * 1e-3) / 1e9, 1),
         "l2_peak_gbps": L2_PEAK_GBPS,
     }
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
         out["cpu_baseline"] = cpu_baseline(pt, scene, info.width, info.height)
     print(json.dumps(out), flush=True)
-    for x in (r, sb, dscene):
-        x.close()
-    if comm is not None:
-        comm.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    shutdown()
 
 
 if __name__ == "__main__":
