@@ -100,6 +100,10 @@ def main():
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # PT_BENCH_REHEARSAL=1: rehearse the multi-rank flow on ONE GPU (every
+    # rank on device 0, frame-end reduce through gloo on host copies, since
+    # RCCL refuses two ranks on one device).  Never used for reported numbers.
+    rehearsal = os.environ.get("PT_BENCH_REHEARSAL") == "1"
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -113,7 +117,7 @@ def main():
     info = scene.info
     width, height = info.width, info.height * world
 
-    dev = pt.Device(local_rank)
+    dev = pt.Device(0 if rehearsal else local_rank)
     dscene = pt.DeviceScene(dev)
     dscene.update(scene)
     sb = pt.SampleBuffer(dev, width, height)
@@ -121,7 +125,7 @@ def main():
     r.RenderFlags = info.render_flags
     r.PathTerminationProbability = info.termination_probability
     comm = None
-    if world > 1:
+    if world > 1 and not rehearsal:
         import torch
         uid = bytearray(pt.Comm.unique_id()) if rank == 0 else bytearray(128)
         t = torch.tensor(list(uid), dtype=torch.uint8)
@@ -149,6 +153,12 @@ def main():
         r.run(1)
     if comm is not None:
         comm.reduce_sample_buffer(sb, 0)
+    elif world > 1:
+        import torch
+        t = torch.from_numpy(sb.read())
+        dist.reduce(t, 0, op=dist.ReduceOp.SUM)
+        if rank == 0:
+            sb.write(t.numpy())
     dev.synchronize()
     barrier()
     dt = time.perf_counter() - t0
@@ -161,7 +171,7 @@ def main():
     trav = r.extend_stats()
     slots_owned = int(np.sum(pt.owned_pixels(width, height, rank, world)))
     acc = sb.read()
-    if comm is None:
+    if world == 1:
         samples = float(acc[..., 3].sum(dtype=np.float64)) - alpha0
     else:
         samples = None   # computed below from the per-rank counts
@@ -222,7 +232,8 @@ def main():
                         f"one round (extend+shade) per step, 16-row bands over {world} GPU(s)",
             "spp_target": info.spp,
             "mesh_faces": info.mesh_face_count,
-            "parallelism": f"pixel-bands x{world}" + (" + RCCL reduce" if world > 1 else ""),
+            "parallelism": f"pixel-bands x{world}" + ((" + gloo reduce (rehearsal, 1 GPU)" if rehearsal
+                                                        else " + RCCL reduce") if world > 1 else ""),
         },
         "msamples_per_s": round(samples / dt / 1e6, 3) if samples is not None else None,
         "roofline": {
