@@ -85,10 +85,11 @@ struct mat4 {
 
 inline vec4 operator*(const mat4& m, vec4 v)
 {
-    // glm: m[0]*v[0] + m[1]*v[1] + m[2]*v[2] + m[3]*v[3]
+    // glm (type_mat4x4.inl, operator*(mat4, vec4)): Add0 = m[0]*v[0] + m[1]*v[1],
+    // Add1 = m[2]*v[2] + m[3]*v[3], result = Add0 + Add1 (pairwise).
     vec4 r;
     for (int i = 0; i < 4; i++)
-        r[i] = m[0][i] * v[0] + m[1][i] * v[1] + m[2][i] * v[2] + m[3][i] * v[3];
+        r[i] = (m[0][i] * v[0] + m[1][i] * v[1]) + (m[2][i] * v[2] + m[3][i] * v[3]);
     return r;
 }
 
