@@ -33,6 +33,7 @@ typedef struct pts_entity pts_entity;
 typedef struct pts_material pts_material;
 typedef struct pts_texture pts_texture;
 typedef struct pts_mesh pts_mesh;
+typedef struct pts_prefab pts_prefab;
 
 enum {   /* entity_type, scene.hpp:228-238 */
     PTS_ENTITY_ROOT = 0,
@@ -62,6 +63,16 @@ typedef struct pts_config_info {
     uint32_t mesh_face_count;
     uint32_t shape_count;
 } pts_config_info;
+
+/* load_model_options (scene.hpp:383-391). */
+typedef struct pts_load_model_options {
+    const char* name;                     /* NULL: file stem */
+    const char* directory_path;           /* NULL: "." (textures and .mtl are looked up here) */
+    float vertex_transform[16];           /* mat4, column-major */
+    float normal_transform[16];
+    float texcoord_transform[9];          /* mat3, column-major */
+    int   openpbr_as_diffuse;             /* extension: BasicDiffuse instead of OpenPBR (K9) */
+} pts_load_model_options;
 
 const char* ptsGetLastError(void);
 
@@ -106,6 +117,21 @@ uint32_t  ptsMeshDepth(pts_mesh* mesh);
 uint32_t  ptsMeshNodeCount(pts_mesh* mesh);
 /* Face vertex indices in BVH order (3 per face). */
 void      ptsMeshFaces(pts_mesh* mesh, uint32_t* indices);
+
+/* Scene ingestion: LoadTexture (scene.cpp:294-313; PNG / Radiance HDR with
+ * stbi_loadf semantics), LoadModelAsPrefab (scene.cpp:601-903; Wavefront
+ * OBJ + MTL), CreateEntity(Scene, Prefab, Parent) (scene.cpp:251-254). */
+void        ptsDefaultLoadModelOptions(pts_load_model_options* options);
+pts_texture* ptsLoadTexture(pts_scene* scene, const char* path, int type, const char* name);
+pts_prefab* ptsLoadModelAsPrefab(pts_scene* scene, const char* path, const pts_load_model_options* options);
+pts_entity* ptsInstantiatePrefab(pts_scene* scene, pts_prefab* prefab, pts_entity* parent);
+uint32_t    ptsPrefabMeshCount(pts_prefab* prefab);
+pts_mesh*   ptsPrefabMesh(pts_prefab* prefab, uint32_t index, pts_material** material, float position[3]);
+uint32_t    ptsMeshVertexCount(pts_mesh* mesh);
+uint32_t    ptsMeshFaceCount(pts_mesh* mesh);
+/* vertices: 8 floats each (position, normal, uv). */
+void        ptsMeshVertices(pts_mesh* mesh, float* vertices);
+int         ptsMaterialType(pts_material* material);
 
 uint32_t ptsPackSceneData(pts_scene* scene);
 void     ptsGetScenePacks(pts_scene* scene, pt_scene_packs* out);

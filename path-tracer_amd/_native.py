@@ -49,6 +49,15 @@ class pt_basic_renderer_params(C.Structure):
     ]
 
 
+class pts_load_model_options(C.Structure):
+    """load_model_options (src/scene/scene.hpp:383-391) + openpbr_as_diffuse."""
+    _fields_ = [
+        ("name", C.c_char_p), ("directory_path", C.c_char_p),
+        ("vertex_transform", C.c_float * 16), ("normal_transform", C.c_float * 16),
+        ("texcoord_transform", C.c_float * 9), ("openpbr_as_diffuse", C.c_int),
+    ]
+
+
 class pt_resolve_parameters(C.Structure):
     """resolve_parameters (src/integrator/integrator.hpp:43-48)."""
     _fields_ = [
@@ -170,6 +179,16 @@ SCENE_API = {
     "ptsMeshDepth": (_u32, [_vp]),
     "ptsMeshNodeCount": (_u32, [_vp]),
     "ptsMeshFaces": (None, [_vp, _u32ptr]),
+    "ptsDefaultLoadModelOptions": (None, [C.POINTER(pts_load_model_options)]),
+    "ptsLoadTexture": (_vp, [_vp, C.c_char_p, _i32, C.c_char_p]),
+    "ptsLoadModelAsPrefab": (_vp, [_vp, C.c_char_p, C.POINTER(pts_load_model_options)]),
+    "ptsInstantiatePrefab": (_vp, [_vp, _vp, _vp]),
+    "ptsPrefabMeshCount": (_u32, [_vp]),
+    "ptsPrefabMesh": (_vp, [_vp, _u32, C.POINTER(_vp), _fptr]),
+    "ptsMeshVertexCount": (_u32, [_vp]),
+    "ptsMeshFaceCount": (_u32, [_vp]),
+    "ptsMeshVertices": (None, [_vp, _fptr]),
+    "ptsMaterialType": (_i32, [_vp]),
     "ptsPackSceneData": (_u32, [_vp]),
     "ptsGetScenePacks": (None, [_vp, C.POINTER(pt_scene_packs)]),
     "ptsMarkDirty": (None, [_vp, _u32]),

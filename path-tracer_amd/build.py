@@ -49,7 +49,7 @@ def build_scene(force=False, verbose=True):
     if not force and not _stale(SCENE_LIB, SCENE_SRC + SCENE_HDR + [Path(__file__)]):
         return SCENE_LIB
     cmd = ["g++", "-std=c++17", "-O2", "-fPIC", "-shared", "-ffp-contract=off", "-Wall",
-           "-Wno-unused-function", "-o", SCENE_LIB] + SCENE_SRC + ["-lpthread"]
+           "-Wno-unused-function", "-o", SCENE_LIB] + SCENE_SRC + ["-lpthread", "-lz"]
     _run(cmd, verbose)
     return SCENE_LIB
 

@@ -6,6 +6,7 @@
 
 #include <cstring>
 #include <string>
+#include <vector>
 
 using namespace pth;
 
@@ -185,6 +186,90 @@ void ptsMeshFaces(pts_mesh* m, uint32_t* out)
     for (size_t f = 0; f < Me(m)->Faces.size(); f++)
         for (int j = 0; j < 3; j++) out[3 * f + j] = Me(m)->Faces[f].VertexIndex[j];
 }
+
+void ptsDefaultLoadModelOptions(pts_load_model_options* o)
+{
+    std::memset(o, 0, sizeof(*o));
+    for (int i = 0; i < 4; i++) { o->vertex_transform[5 * i] = 1; o->normal_transform[5 * i] = 1; }
+    for (int i = 0; i < 3; i++) o->texcoord_transform[4 * i] = 1;
+}
+
+pts_texture* ptsLoadTexture(pts_scene* s, const char* path, int type, const char* name)
+{
+    std::string err;
+    texture* t = LoadTexture(S(s), path, (uint32_t)type, name, &err);
+    if (!t) g_err = "LoadTexture: " + err;
+    return reinterpret_cast<pts_texture*>(t);
+}
+
+pts_prefab* ptsLoadModelAsPrefab(pts_scene* s, const char* path, const pts_load_model_options* o)
+{
+    load_model_options opt;
+    if (o) {
+        if (o->name) opt.Name = o->name;
+        if (o->directory_path) opt.DirectoryPath = o->directory_path;
+        for (int c = 0; c < 4; c++)
+            for (int r = 0; r < 4; r++) {
+                opt.VertexTransform[c][r] = o->vertex_transform[4 * c + r];
+                opt.NormalTransform[c][r] = o->normal_transform[4 * c + r];
+            }
+        for (int i = 0; i < 9; i++) opt.TextureCoordinateTransform[i] = o->texcoord_transform[i];
+        opt.OpenPBRAsDiffuse = o->openpbr_as_diffuse != 0;
+    }
+    std::string err;
+    prefab* p = LoadModelAsPrefab(S(s), path, &opt, &err);
+    if (!p) g_err = "LoadModelAsPrefab: " + err;
+    return reinterpret_cast<pts_prefab*>(p);
+}
+
+pts_entity* ptsInstantiatePrefab(pts_scene* s, pts_prefab* p, pts_entity* parent)
+{
+    return reinterpret_cast<pts_entity*>(
+        CreateEntity(S(s), reinterpret_cast<prefab*>(p), reinterpret_cast<entity*>(parent)));
+}
+
+static void CollectMeshes(entity* e, std::vector<entity*>& out)
+{
+    if (e->Type == ENTITY_TYPE_MESH_INSTANCE) out.push_back(e);
+    for (entity* c : e->Children) CollectMeshes(c, out);
+}
+
+uint32_t ptsPrefabMeshCount(pts_prefab* p)
+{
+    std::vector<entity*> m;
+    CollectMeshes(reinterpret_cast<prefab*>(p)->Entity, m);
+    return (uint32_t)m.size();
+}
+
+pts_mesh* ptsPrefabMesh(pts_prefab* p, uint32_t index, pts_material** material, float position[3])
+{
+    std::vector<entity*> m;
+    CollectMeshes(reinterpret_cast<prefab*>(p)->Entity, m);
+    if (index >= m.size()) return nullptr;
+    if (material) *material = reinterpret_cast<pts_material*>(m[index]->Material);
+    if (position) {
+        position[0] = m[index]->Transform.Position.x;
+        position[1] = m[index]->Transform.Position.y;
+        position[2] = m[index]->Transform.Position.z;
+    }
+    return reinterpret_cast<pts_mesh*>(m[index]->Mesh);
+}
+
+uint32_t ptsMeshVertexCount(pts_mesh* m) { return (uint32_t)Me(m)->Vertices.size(); }
+uint32_t ptsMeshFaceCount(pts_mesh* m) { return (uint32_t)Me(m)->Faces.size(); }
+
+void ptsMeshVertices(pts_mesh* m, float* out)
+{
+    for (size_t i = 0; i < Me(m)->Vertices.size(); i++) {
+        const mesh_vertex& v = Me(m)->Vertices[i];
+        float* o = out + 8 * i;
+        o[0] = v.Position.x; o[1] = v.Position.y; o[2] = v.Position.z;
+        o[3] = v.Normal.x; o[4] = v.Normal.y; o[5] = v.Normal.z;
+        o[6] = v.UV.x; o[7] = v.UV.y;
+    }
+}
+
+int ptsMaterialType(pts_material* m) { return m ? (int)reinterpret_cast<material*>(m)->Type : -1; }
 
 uint32_t ptsPackSceneData(pts_scene* s) { return PackSceneData(S(s)); }
 void ptsGetScenePacks(pts_scene* s, pt_scene_packs* out) { GetScenePacks(S(s), out); }

@@ -1,0 +1,19 @@
+// image.hpp — texture file decoding (PNG, Radiance HDR) for LoadTexture.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "hmath.hpp"
+
+namespace pth {
+
+// stbi_loadf(path, ..., 4) semantics: RGBA floats, LDR colour channels
+// linearised by pow(v / 255, 2.2), alpha v / 255; HDR decoded linearly.
+bool LoadImageFloat(const char* Path, int& Width, int& Height, std::vector<vec4>& Pixels, std::string& Error);
+
+// The 8-bit RGBA samples of a PNG (before linearisation), for tests.
+bool LoadImageRGBA8(const char* Path, int& Width, int& Height, std::vector<uint8_t>& RGBA, std::string& Error);
+
+}  // namespace pth

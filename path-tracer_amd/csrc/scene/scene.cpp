@@ -259,6 +259,7 @@ scene::~scene()
     for (mesh* M : Meshes) delete M;
     for (material* M : Materials) delete M;
     for (texture* T : Textures) delete T;
+    for (prefab* P : Prefabs) delete P;
 }
 
 scene* CreateEmptyScene()

@@ -150,12 +150,30 @@ struct entity {                       // scene.hpp:240-252 (+ subtype fields)
     mesh* Mesh = nullptr;
 };
 
+struct prefab {                       // scene.hpp:318-321
+    entity* Entity = nullptr;
+    std::vector<entity*> Owned;       // the prefab's own entity tree (not in the scene)
+    ~prefab() { for (entity* E : Owned) delete E; }
+};
+
+struct load_model_options {           // scene.hpp:383-391
+    std::string Name;                 // empty: file stem
+    std::string DirectoryPath = ".";
+    mat4 VertexTransform = mat4(1.0f);
+    mat4 NormalTransform = mat4(1.0f);
+    float TextureCoordinateTransform[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};   // mat3, column-major
+    // Extension: create BasicDiffuse (Kd + map_Kd) instead of the reference's
+    // OpenPBR materials, which its integrator does not shade.
+    bool OpenPBRAsDiffuse = false;
+};
+
 struct scene {                        // scene.hpp:335-362
     entity Root;
     std::vector<entity*> Entities;    // ownership of every non-root entity
     std::vector<mesh*> Meshes;
     std::vector<material*> Materials;
     std::vector<texture*> Textures;
+    std::vector<prefab*> Prefabs;
     parametric_spectrum_table* RGBSpectrumTable = nullptr;
 
     // Packed data (PackSceneData).
@@ -192,6 +210,12 @@ texture* CreateTexture(scene* Scene, const char* Name, uint32_t Type, uint32_t W
 mesh* CreateMesh(scene* Scene, const char* Name, uint32_t VertexCount, const float* Positions,
                  const float* Normals, const float* UVs, uint32_t FaceCount, const uint32_t* Indices);
 void BuildMeshBVH(mesh* Mesh);
+
+// Scene ingestion (import.cpp).
+texture* LoadTexture(scene* Scene, const char* Path, uint32_t Type, const char* Name, std::string* Error);
+prefab* LoadModelAsPrefab(scene* Scene, const char* Path, const load_model_options* Options, std::string* Error);
+entity* CreateEntity(scene* Scene, const entity* Source, entity* Parent);
+entity* CreateEntity(scene* Scene, const prefab* Prefab, entity* Parent);
 
 uint32_t PackSceneData(scene* Scene);
 void GetScenePacks(scene* Scene, pt_scene_packs* Out);

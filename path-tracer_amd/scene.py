@@ -7,6 +7,7 @@ keeping the reference's names and field meanings.
 from __future__ import annotations
 
 import ctypes as C
+from pathlib import Path
 
 import numpy as np
 
@@ -143,6 +144,58 @@ class Scene:
         if not m:
             raise ValueError(L.ptsGetLastError().decode())
         return m
+
+    # -- ingestion (scene.cpp:294-313, 601-903) ---------------------------------
+    def load_texture(self, path, texture_type=TEXTURE_RAW, name=None):
+        """LoadTexture: PNG or Radiance .hdr, stbi_loadf semantics."""
+        L = N.scene_lib()
+        t = L.ptsLoadTexture(self._h, str(path).encode(), int(texture_type), name.encode() if name else None)
+        if not t:
+            raise OSError(L.ptsGetLastError().decode())
+        return t
+
+    def load_model_as_prefab(self, path, name=None, directory=None, vertex_transform=None, normal_transform=None,
+                             texcoord_transform=None, openpbr_as_diffuse=False):
+        """LoadModelAsPrefab (Wavefront OBJ + MTL).  Transforms are 4x4 / 3x3
+        arrays (column vectors, like glm); directory defaults to the OBJ's."""
+        L = N.scene_lib()
+        o = N.pts_load_model_options()
+        L.ptsDefaultLoadModelOptions(C.byref(o))
+        o.name = name.encode() if name else None
+        o.directory_path = str(directory if directory is not None else Path(path).parent).encode()
+        for field, m, n in (("vertex_transform", vertex_transform, 4), ("normal_transform", normal_transform, 4),
+                            ("texcoord_transform", texcoord_transform, 3)):
+            if m is not None:
+                a = np.asarray(m, dtype=np.float32).reshape(n, n).T.reshape(-1)   # column-major
+                getattr(o, field)[:] = [float(x) for x in a]
+        o.openpbr_as_diffuse = int(bool(openpbr_as_diffuse))
+        p = L.ptsLoadModelAsPrefab(self._h, str(path).encode(), C.byref(o))
+        if not p:
+            raise OSError(L.ptsGetLastError().decode())
+        return p
+
+    def instantiate_prefab(self, prefab, parent=None):
+        """CreateEntity(Scene, Prefab, Parent): deep copy into the scene."""
+        return N.scene_lib().ptsInstantiatePrefab(self._h, prefab, parent)
+
+    @staticmethod
+    def prefab_meshes(prefab):
+        """[(vertices (n, 8): position/normal/uv, faces (m, 3), material type, instance position)]."""
+        L = N.scene_lib()
+        out = []
+        for i in range(L.ptsPrefabMeshCount(prefab)):
+            mat = C.c_void_p()
+            pos = np.zeros(3, dtype=np.float32)
+            m = L.ptsPrefabMesh(prefab, i, C.byref(mat), N.fptr(pos))
+            nv, nf = L.ptsMeshVertexCount(m), L.ptsMeshFaceCount(m)
+            v = np.zeros((nv, 8), dtype=np.float32)
+            f = np.zeros((nf, 3), dtype=np.uint32)
+            if nv:
+                L.ptsMeshVertices(m, N.fptr(v))
+            if nf:
+                L.ptsMeshFaces(m, N.u32ptr(f))
+            out.append((v, f, L.ptsMaterialType(mat) if mat.value else None, pos))
+        return out
 
     # -- packing -------------------------------------------------------------
     def pack(self) -> int:
