@@ -215,8 +215,11 @@ int ptCheckFastDivision(pt_device* device, uint64_t n, uint32_t seed, uint64_t* 
 /* Diagnostic: runs the extend step on the renderer's current rays with
  * traversal counters.  It writes the same hit records the next Run's extend
  * writes first, so the render is not perturbed.  out = {rays, lane steps, wave steps x 64, internal nodes,
- * BLAS leaves, faces tested, stack pops, TLAS leaves, waves}. */
-int ptExtendStats(pt_device* device, pt_basic_renderer* renderer, uint64_t out[9]);
+ * BLAS leaves, faces tested, stack pops, TLAS leaves, waves, then the internal
+ * BLAS wave steps by the number of distinct nodes among the wave's lanes
+ * taking them: 1, 2, 3-4, 5-8, more than 8}. */
+#define PT_EXTEND_STATS_COUNT 14
+int ptExtendStats(pt_device* device, pt_basic_renderer* renderer, uint64_t out[PT_EXTEND_STATS_COUNT]);
 
 /* Per-kernel device time, measured with HIP events on the renderer stream. */
 int ptSetProfiling(pt_device* device, int enable);

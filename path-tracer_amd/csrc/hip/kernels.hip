@@ -555,7 +555,8 @@ PT_DEV uint32_t WaveMax(uint32_t v)
 
 // Diagnostic extend: the same traversal with per-lane counters, reduced per
 // wave into out[]: {rays, lane steps, wave steps x 64, internal nodes, BLAS
-// leaves, faces tested, stack pops, TLAS leaves (shapes), waves}.  SIMD
+// leaves, faces tested, stack pops, TLAS leaves (shapes), waves, then the
+// internal-BLAS wave steps by distinct node count 1, 2, 3-4, 5-8, >8}.  SIMD
 // efficiency of the traversal loop = lane steps / (wave steps x 64).
 template <class Src, bool SPILL, int CAP>
 __global__ __launch_bounds__(256) void extend_stats_kernel(dscene S, Src src, uint32_t n, uint32_t* spill,
@@ -579,10 +580,12 @@ __global__ __launch_bounds__(256) void extend_stats_kernel(dscene S, Src src, ui
             while (!LaneStep<SPILL, CAP>(S, Ln, st, src, slot, ss)) {}
         src.store(slot, Ln);
     }
-    uint32_t v[9] = {WaveSum(ray), WaveSum(ss.steps), WaveMax(ss.steps) * 64u, WaveSum(ss.internals),
-                     WaveSum(ss.leaves), WaveSum(ss.faces), WaveSum(ss.pops), WaveSum(ss.shapes), 1u};
+    uint32_t v[14] = {WaveSum(ray), WaveSum(ss.steps), WaveMax(ss.steps) * 64u, WaveSum(ss.internals),
+                      WaveSum(ss.leaves), WaveSum(ss.faces), WaveSum(ss.pops), WaveSum(ss.shapes), 1u,
+                      WaveSum(ss.uniq[0]), WaveSum(ss.uniq[1]), WaveSum(ss.uniq[2]), WaveSum(ss.uniq[3]),
+                      WaveSum(ss.uniq[4])};
     if ((threadIdx.x & 63u) == 0)
-        for (int i = 0; i < 9; i++) atomicAdd(&out[i], (unsigned long long)v[i]);
+        for (int i = 0; i < 14; i++) atomicAdd(&out[i], (unsigned long long)v[i]);
 }
 
 // Compact hit -> the reference's packed trace record (StoreTraceHit,

@@ -895,22 +895,22 @@ int ptCheckFastDivision(pt_device* d, uint64_t n, uint32_t seed, uint64_t* misma
     return 0;
 }
 
-int ptExtendStats(pt_device* d, pt_basic_renderer* r, uint64_t out[9])
+int ptExtendStats(pt_device* d, pt_basic_renderer* r, uint64_t out[PT_EXTEND_STATS_COUNT])
 {
     if (!d || !out) { SetError("null argument"); return -1; }
     if (CheckReady(r) != 0) return -1;
     PT_HIP(hipSetDevice(d->id));
     if (int e = EnsureSpill(r)) return e;
     unsigned long long* dm = nullptr;
-    PT_HIP(hipMalloc(&dm, 9 * sizeof(unsigned long long)));
-    hipError_t e = hipMemsetAsync(dm, 0, 9 * sizeof(unsigned long long), d->stream);
+    PT_HIP(hipMalloc(&dm, PT_EXTEND_STATS_COUNT * sizeof(unsigned long long)));
+    hipError_t e = hipMemsetAsync(dm, 0, PT_EXTEND_STATS_COUNT * sizeof(unsigned long long), d->stream);
     if (e == hipSuccess) e = pt_launch_extend_stats(r->scene->d, r->slots, Frame(r), r->slots.spill, dm, d->stream);
-    unsigned long long h[9] = {};
+    unsigned long long h[PT_EXTEND_STATS_COUNT] = {};
     if (e == hipSuccess) e = hipMemcpyAsync(h, dm, sizeof(h), hipMemcpyDeviceToHost, d->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
     (void)hipFree(dm);
     if (e != hipSuccess) { SetError("ptExtendStats: %s", hipGetErrorString(e)); return (int)e; }
-    for (int i = 0; i < 9; i++) out[i] = h[i];
+    for (int i = 0; i < PT_EXTEND_STATS_COUNT; i++) out[i] = h[i];
     return 0;
 }
 

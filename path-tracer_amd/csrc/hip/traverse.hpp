@@ -143,6 +143,7 @@ PT_DEV void LaneMeshFace(const dscene& S, uint32_t F, lane_state& L)
 // Traversal statistics hooks: no-ops in the render kernel, counters in the
 // diagnostic instantiation (ptExtendStats).
 struct no_stats {
+    PT_DEV void coherence(uint32_t) {}
     PT_DEV void node(bool) {}
     PT_DEV void step() {}
     PT_DEV void internal() {}
@@ -152,6 +153,26 @@ struct no_stats {
 };
 struct lane_stats {
     uint32_t steps = 0, internals = 0, leaves = 0, faces = 0, shapes = 0, pops = 0;
+    // Wave coherence of internal BLAS steps: wave steps by the number of
+    // distinct nodes among the lanes taking the step {1, 2, 3-4, 5-8, >8},
+    // counted on the first such lane.
+    uint32_t uniq[5] = {0, 0, 0, 0, 0};
+    PT_DEV void coherence(uint32_t index)
+    {
+        uint64_t act = __ballot(1);
+        uint32_t first = (uint32_t)__ffsll((long long)act) - 1u;
+        uint32_t lane = __lane_id();
+        uint32_t u = 0;
+        bool done = false;
+        for (;;) {
+            uint64_t m = __ballot(!done);
+            if (m == 0) break;
+            uint32_t f = (uint32_t)__shfl(index, (int)(__ffsll((long long)m) - 1), 64);
+            if (!done && index == f) done = true;
+            u++;
+        }
+        if (lane == first) uniq[u == 1 ? 0 : u == 2 ? 1 : u <= 4 ? 2 : u <= 8 ? 3 : 4]++;
+    }
     PT_DEV void node(bool) {}
     PT_DEV void step() { steps++; }
     PT_DEV void internal() { internals++; }
@@ -185,6 +206,7 @@ PT_DEV void UnpackBlasEntry(uint32_t e, uint32_t& na, uint32_t& nb)
 // per Intersect / IntersectMeshNode loop iteration = one LaneStep at that level.
 struct complexity_stats {
     uint32_t scene = 0, mesh = 0;
+    PT_DEV void coherence(uint32_t) {}
     PT_DEV void node(bool blas) { if (blas) mesh++; else scene++; }
     PT_DEV void step() {}
     PT_DEV void internal() {}
@@ -212,6 +234,7 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
         } else {
             ss.internal();
             uint32_t Index = L.na;
+            ss.coherence(Index);
             float4 a0 = S.mesh_nodes[2 * Index], a1 = S.mesh_nodes[2 * Index + 1];
             float4 b0 = S.mesh_nodes[2 * Index + 2], b1 = S.mesh_nodes[2 * Index + 3];
             float TA = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, a0, a1, L.exact);

@@ -213,10 +213,11 @@ class BasicRenderer:
 
     def extend_stats(self) -> dict:
         """Traversal counters of the current rays (diagnostic, ptExtendStats)."""
-        out = (C.c_uint64 * 9)()
+        out = (C.c_uint64 * 14)()
         _check(N.hip_lib().ptExtendStats(self.device.handle, self._h, out), "ptExtendStats")
         keys = ("rays", "lane_steps", "wave_steps_x64", "internal_nodes", "blas_leaves", "faces", "pops",
-                "tlas_leaves", "waves")
+                "tlas_leaves", "waves", "blas_steps_distinct1", "blas_steps_distinct2", "blas_steps_distinct3_4",
+                "blas_steps_distinct5_8", "blas_steps_distinct9_")
         d = dict(zip(keys, (int(x) for x in out)))
         d["simd_efficiency"] = d["lane_steps"] / max(d["wave_steps_x64"], 1)
         for k in ("lane_steps", "internal_nodes", "blas_leaves", "faces", "pops", "tlas_leaves"):
