@@ -537,7 +537,7 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
     LaneBegin(S, Ln, O, V, D);
     no_stats ns;
     if (S.g.ShapeCount != 0)
-        while (!LaneStep<SPILL, CAP>(S, Ln, st, src, slot, ns)) {}
+        while (!LaneStep<SPILL, CAP, Src, no_stats, true>(S, Ln, st, src, slot, ns)) {}
     src.store(slot, Ln);
 }
 
@@ -577,7 +577,7 @@ __global__ __launch_bounds__(256) void extend_stats_kernel(dscene S, Src src, ui
         lane_state Ln;
         LaneBegin(S, Ln, O, V, D);
         if (S.g.ShapeCount != 0)
-            while (!LaneStep<SPILL, CAP>(S, Ln, st, src, slot, ss)) {}
+            while (!LaneStep<SPILL, CAP, Src, lane_stats, true>(S, Ln, st, src, slot, ss)) {}
         src.store(slot, Ln);
     }
     uint32_t v[14] = {WaveSum(ray), WaveSum(ss.steps), WaveMax(ss.steps) * 64u, WaveSum(ss.internals),

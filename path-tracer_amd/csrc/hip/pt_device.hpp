@@ -27,7 +27,7 @@ struct dscene {
     const uint32_t* material;
     const pt_packed_shape* shapes;
     const float4* shape_nodes;     // 2 x float4 per node
-    const float4* mesh_faces;      // 3 x float4 per face
+    const float4* mesh_faces;      // 3 x float4 per face: {Position0, Edge1, Edge2}, .w = vertex indices
     const uint2* mesh_vertices;
     const float4* mesh_nodes;      // 2 x float4 per node
     const pt_packed_camera* cameras;
@@ -168,20 +168,13 @@ PT_DEV bool FastDivRay(pt3 O, pt3 V)
     return ok;
 }
 
-PT_DEV float HwMin(float a, float b) { float r; asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
-PT_DEV float HwMax(float a, float b) { float r; asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
-PT_DEV float HwMin3(float a, float b, float c)
-{
-    float r;
-    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-PT_DEV float HwMax3(float a, float b, float c)
-{
-    float r;
-    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
+// Operands are results of arithmetic (never signalling NaNs), so minnum /
+// maxnum lower to bare v_min/v_max (+ v_min3/v_max3) with no canonicalising
+// moves, and the scheduler may interleave them with the divisions.
+PT_DEV float HwMin(float a, float b) { return __builtin_fminf(a, b); }
+PT_DEV float HwMax(float a, float b) { return __builtin_fmaxf(a, b); }
+PT_DEV float HwMin3(float a, float b, float c) { return __builtin_fminf(__builtin_fminf(a, b), c); }
+PT_DEV float HwMax3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
 
 PT_DEV float FastQuot(float a, float b, float y)
 {

@@ -479,7 +479,17 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
         PT_HIP(s->shape_nodes.upload(p->shape_nodes, p->shape_node_count));
     }
     if (first || (dirty & PT_SCENE_DIRTY_MESHES)) {
-        PT_HIP(s->faces.upload(p->mesh_faces, p->mesh_face_count));
+        // Device face records carry {Position0, Edge1, Edge2} (traverse.hpp
+        // LaneMeshFace): the reference's per-test edge subtractions
+        // (scene.glsl.inc:307-308) done once here, same IEEE f32 operations.
+        std::vector<pt_packed_mesh_face> ef(p->mesh_faces, p->mesh_faces + p->mesh_face_count);
+        for (pt_packed_mesh_face& F : ef)
+            for (int k = 0; k < 3; k++) {
+                float p0 = F.Position0[k];
+                F.Position1[k] = F.Position1[k] - p0;
+                F.Position2[k] = F.Position2[k] - p0;
+            }
+        PT_HIP(s->faces.upload(ef.data(), ef.size()));
         PT_HIP(s->vertices.upload(p->mesh_vertices, p->mesh_vertex_count));
         PT_HIP(s->mesh_nodes.upload(p->mesh_nodes, p->mesh_node_count));
     }

@@ -116,12 +116,16 @@ PT_DEV void IntersectAnalytic(int32_t Type, pt3 O, pt3 V, uint32_t ShapeIndex, l
 }
 
 // IntersectMeshFace (scene.glsl.inc:304-334) on the lane's object-space ray.
+// The device face array holds {Position0, Edge1, Edge2} (dscene::mesh_faces):
+// the edges are the reference's `Position1 - Position0`, `Position2 -
+// Position0`, subtracted once on the host at upload in the same IEEE
+// arithmetic, so every later operation sees identical operands.
 PT_DEV void LaneMeshFace(const dscene& S, uint32_t F, lane_state& L)
 {
     float4 a = S.mesh_faces[3 * F + 0], b = S.mesh_faces[3 * F + 1], c = S.mesh_faces[3 * F + 2];
     pt3 P0 = xyz(a);
-    pt3 Edge1 = xyz(b) - P0;
-    pt3 Edge2 = xyz(c) - P0;
+    pt3 Edge1 = xyz(b);
+    pt3 Edge2 = xyz(c);
     pt3 RCE2 = cross(L.V, Edge2);
     float Det = dot(Edge1, RCE2);
     if (pt_abs(Det) < PT_EPSILON) return;
@@ -143,6 +147,7 @@ PT_DEV void LaneMeshFace(const dscene& S, uint32_t F, lane_state& L)
 // Traversal statistics hooks: no-ops in the render kernel, counters in the
 // diagnostic instantiation (ptExtendStats).
 struct no_stats {
+    PT_DEV void face_step(bool) {}
     PT_DEV void coherence(uint32_t) {}
     PT_DEV void node(bool) {}
     PT_DEV void step() {}
@@ -177,6 +182,8 @@ struct lane_stats {
     PT_DEV void step() { steps++; }
     PT_DEV void internal() { internals++; }
     PT_DEV void leaf(uint32_t n) { leaves++; faces += n; }
+    // FACE_STEP leaves: one call per face; the leaf counts once, on its last.
+    PT_DEV void face_step(bool last) { faces++; leaves += last; }
     PT_DEV void shape() { shapes++; }
     PT_DEV void pop() { pops++; }
 };
@@ -207,6 +214,7 @@ PT_DEV void UnpackBlasEntry(uint32_t e, uint32_t& na, uint32_t& nb)
 struct complexity_stats {
     uint32_t scene = 0, mesh = 0;
     PT_DEV void coherence(uint32_t) {}
+    PT_DEV void face_step(bool last) { mesh += last; }
     PT_DEV void node(bool blas) { if (blas) mesh++; else scene++; }
     PT_DEV void step() {}
     PT_DEV void internal() {}
@@ -218,20 +226,38 @@ struct complexity_stats {
 // Advances one lane by one node.  Returns true when its Trace() is complete.
 // Only the two index words of the current node are carried between steps;
 // its bounds were already consumed by the parent's box test.
-template <bool SPILL, int CAP, class Src, class Stats = no_stats>
+//
+// FACE_STEP: a BLAS leaf advances by ONE face per step (na walks up to nb), so
+// a divergent wave step costs one face test beside the internal-node lanes'
+// box tests instead of the longest leaf's whole face loop.  The faces are
+// still tested in the reference's order, each with the Hit.Time left by the
+// previous one, and the pop follows the last face, so results are identical.
+template <bool SPILL, int CAP, class Src, class Stats = no_stats, bool FACE_STEP = false>
 PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, const Src& src, uint32_t slot,
                      Stats& ss)
 {
-    ss.node(L.blas != SHAPE_INDEX_NONE);
     ss.step();
     const uint32_t* mesh_words = reinterpret_cast<const uint32_t*>(S.mesh_nodes);
     const uint32_t* shape_words = reinterpret_cast<const uint32_t*>(S.shape_nodes);
     if (L.blas != SHAPE_INDEX_NONE) {
         // IntersectMeshNode (scene.glsl.inc:336-399), one node.
         if (L.nb > 0) {
-            ss.leaf(L.nb - L.na);
-            for (uint32_t F = L.na; F < L.nb; F++) LaneMeshFace(S, F, L);
+            if (FACE_STEP) {
+                if (L.na < L.nb) {
+                    LaneMeshFace(S, L.na, L);
+                    bool last = ++L.na == L.nb;
+                    ss.face_step(last);
+                    if (!last) return false;
+                } else {
+                    ss.face_step(true);
+                }
+            } else {
+                ss.node(true);
+                ss.leaf(L.nb - L.na);
+                for (uint32_t F = L.na; F < L.nb; F++) LaneMeshFace(S, F, L);
+            }
         } else {
+            ss.node(true);
             ss.internal();
             uint32_t Index = L.na;
             ss.coherence(Index);
@@ -277,6 +303,7 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
         SetLevelRay(S, L, WO, WV);
     } else {
         // Intersect (scene.glsl.inc:468-520), one node.
+        ss.node(false);
         uint32_t Children = L.na;
         if (Children == 0) {
             ss.shape();
