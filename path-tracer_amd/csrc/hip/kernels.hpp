@@ -26,6 +26,8 @@ struct dslots {
     float4* prob;       // probability[4]
     float4* smp;        // sample.xyz, normalized lambda0
     uint2* act;         // active-shape stack (2 x u16 pairs)
+    uint16_t* pos;      // per slot: position of its current ray (high byte) and of
+                        // its last traced hit (low byte) within its tile (TileOrder)
     uint32_t* spill;    // traversal stack spill: (needed - LDS capacity) rows x n
     uint32_t n;
 };

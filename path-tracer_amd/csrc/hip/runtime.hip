@@ -135,6 +135,7 @@ struct pt_basic_renderer {
     dbuf<float4> ray, hit, thr, prob, smp;
     dbuf<float2> uv;
     dbuf<uint2> act;
+    dbuf<uint16_t> pos;                 // TileOrder positions (kernels.hip)
     dbuf<uint32_t> spill;
 };
 
@@ -623,16 +624,17 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     uint32_t ns = (uint32_t)n;
     bool ok = r->ray.alloc(ns) == hipSuccess && r->hit.alloc(ns) == hipSuccess && r->thr.alloc(ns) == hipSuccess &&
               r->prob.alloc(ns) == hipSuccess && r->smp.alloc(ns) == hipSuccess && r->uv.alloc(ns) == hipSuccess &&
-              r->act.alloc(ns) == hipSuccess;
+              r->act.alloc(ns) == hipSuccess && r->pos.alloc(ns) == hipSuccess;
     if (ok && ns) {
         ok = hipMemset(r->ray.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->hit.ptr, 0, (size_t)ns * 16) == hipSuccess &&
              hipMemset(r->thr.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->prob.ptr, 0, (size_t)ns * 16) == hipSuccess &&
              hipMemset(r->smp.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->uv.ptr, 0, (size_t)ns * 8) == hipSuccess &&
-             hipMemset(r->act.ptr, 0, (size_t)ns * 8) == hipSuccess;
+             hipMemset(r->act.ptr, 0, (size_t)ns * 8) == hipSuccess && hipMemset(r->pos.ptr, 0, (size_t)ns * 2) == hipSuccess;
     }
     if (!ok) {
         SetError("renderer slot allocation failed (%u slots)", ns);
         r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->smp.release(); r->uv.release(); r->act.release();
+        r->pos.release();
         delete r;
         return nullptr;
     }
@@ -643,6 +645,7 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     r->slots.prob = r->prob.ptr;
     r->slots.smp = r->smp.ptr;
     r->slots.act = r->act.ptr;
+    r->slots.pos = r->pos.ptr;
     r->slots.spill = nullptr;
     r->slots.n = ns;
     return r;
@@ -658,7 +661,7 @@ void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
     if (!r) return;
     if (d) { (void)hipSetDevice(d->id); (void)hipStreamSynchronize(d->stream); }
     r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->smp.release();
-    r->uv.release(); r->act.release(); r->spill.release();
+    r->uv.release(); r->act.release(); r->pos.release(); r->spill.release();
     delete r;
 }
 
@@ -708,6 +711,7 @@ int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state*
     std::vector<float4> ray(n), hit(n), thr(n), prob(n), smp(n);
     std::vector<float2> uv(n);
     std::vector<uint2> act(n);
+    std::vector<uint16_t> pos(n);
     if (n && r->scene->valid) {
         // The slots hold compact hits; rebuild the reference's packed trace
         // records (normal, tangent, uv, material) for the readback.
@@ -728,6 +732,7 @@ int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state*
     PT_HIP(hipMemcpy(prob.data(), r->prob.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
     PT_HIP(hipMemcpy(smp.data(), r->smp.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
     PT_HIP(hipMemcpy(act.data(), r->act.ptr, (size_t)n * 8, hipMemcpyDeviceToHost));
+    PT_HIP(hipMemcpy(pos.data(), r->pos.ptr, (size_t)n * 2, hipMemcpyDeviceToHost));
     uint32_t W = r->buffer->width, H = r->buffer->height;
     auto bits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
     for (uint32_t s = 0; s < n; s++) {
@@ -735,14 +740,16 @@ int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state*
         uint32_t x = tx * 16 + (l & 15u), y = (r->rank + k * r->nranks) * 16 + (l >> 4);
         if (x >= W || y >= H) continue;
         pt_pixel_state& O = out[(size_t)y * W + x];
-        O.origin[0] = ray[s].x; O.origin[1] = ray[s].y; O.origin[2] = ray[s].z;
-        O.packed_velocity = bits(ray[s].w);
-        O.hit.time = hit[s].x;
-        O.hit.shape_material = bits(hit[s].y);
-        O.hit.packed_normal = bits(hit[s].z);
-        O.hit.packed_tangent = bits(hit[s].w);
-        O.hit.u = uv[s].x;
-        O.hit.v = uv[s].y;
+        // Ray and hit records live at the slot's TileOrder positions.
+        uint32_t qr = (s & ~255u) | (pos[s] >> 8u), qh = (s & ~255u) | (pos[s] & 255u);
+        O.origin[0] = ray[qr].x; O.origin[1] = ray[qr].y; O.origin[2] = ray[qr].z;
+        O.packed_velocity = bits(ray[qr].w);
+        O.hit.time = hit[qh].x;
+        O.hit.shape_material = bits(hit[qh].y);
+        O.hit.packed_normal = bits(hit[qh].z);
+        O.hit.packed_tangent = bits(hit[qh].w);
+        O.hit.u = uv[qh].x;
+        O.hit.v = uv[qh].y;
         O.lambda0 = smp[s].w;
         O.throughput[0] = thr[s].x; O.throughput[1] = thr[s].y; O.throughput[2] = thr[s].z; O.throughput[3] = thr[s].w;
         O.probability[0] = prob[s].x; O.probability[1] = prob[s].y; O.probability[2] = prob[s].z; O.probability[3] = prob[s].w;

@@ -79,8 +79,16 @@ def main():
     def coarse(bits):
         return (oct_ << np.uint64(bits - 3)) | (mo >> np.uint64(30 - (bits - 3)))
 
+    # Pixel (x, y) of every ray in slot order; wave footprints other than the
+    # tile layout's 16x4 rows.
+    px, py = x[base], y[base]
+    tile = (py // 16) * (W // 16) + px // 16
+    quad = ((py % 16) // 8) * 2 + (px % 16) // 8
+    in8 = (py % 8) * 8 + px % 8
     orders = {
         "slot": np.arange(n),
+        "wave8x8": np.lexsort((in8, quad, tile)),
+        "wave8x8_z": np.lexsort((morton3(np.stack([px % 8, py % 8, np.zeros_like(px)], 1)), quad, tile)),
         "global_oct_morton": np.lexsort((mo, oct_)),
         "global_morton_origin": np.argsort(mo, kind="stable"),
         "global_bin9": np.argsort(coarse(9), kind="stable"),
