@@ -133,6 +133,16 @@ uint32_t    ptsMeshFaceCount(pts_mesh* mesh);
 void        ptsMeshVertices(pts_mesh* mesh, float* vertices);
 int         ptsMaterialType(pts_material* material);
 
+/* Scene files: LoadScene / SaveScene (serializer.cpp:511-529): <path> is the
+ * scene JSON; textures (<name>.texture), meshes (<name>.mesh) and the
+ * spectrum table (spectrum.dat) sit beside it.  Load returns NULL on error. */
+pts_scene*  ptsLoadScene(const char* path);
+int         ptsSaveScene(pts_scene* scene, const char* path);
+uint32_t    ptsSceneTextureCount(pts_scene* scene);
+uint32_t    ptsSceneMaterialCount(pts_scene* scene);
+uint32_t    ptsSceneMeshCount(pts_scene* scene);
+uint32_t    ptsScenePrefabCount(pts_scene* scene);
+
 uint32_t ptsPackSceneData(pts_scene* scene);
 void     ptsGetScenePacks(pts_scene* scene, pt_scene_packs* out);
 void     ptsMarkDirty(pts_scene* scene, uint32_t flags);

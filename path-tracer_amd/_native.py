@@ -183,6 +183,12 @@ SCENE_API = {
     "ptsLoadTexture": (_vp, [_vp, C.c_char_p, _i32, C.c_char_p]),
     "ptsLoadModelAsPrefab": (_vp, [_vp, C.c_char_p, C.POINTER(pts_load_model_options)]),
     "ptsInstantiatePrefab": (_vp, [_vp, _vp, _vp]),
+    "ptsLoadScene": (_vp, [C.c_char_p]),
+    "ptsSaveScene": (_i32, [_vp, C.c_char_p]),
+    "ptsSceneTextureCount": (_u32, [_vp]),
+    "ptsSceneMaterialCount": (_u32, [_vp]),
+    "ptsSceneMeshCount": (_u32, [_vp]),
+    "ptsScenePrefabCount": (_u32, [_vp]),
     "ptsPrefabMeshCount": (_u32, [_vp]),
     "ptsPrefabMesh": (_vp, [_vp, _u32, C.POINTER(_vp), _fptr]),
     "ptsMeshVertexCount": (_u32, [_vp]),

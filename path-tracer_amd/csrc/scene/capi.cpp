@@ -222,6 +222,28 @@ pts_prefab* ptsLoadModelAsPrefab(pts_scene* s, const char* path, const pts_load_
     return reinterpret_cast<pts_prefab*>(p);
 }
 
+pts_scene* ptsLoadScene(const char* path)
+{
+    if (!path) { g_err = "LoadScene: null path"; return nullptr; }
+    std::string err;
+    scene* sc = LoadScene(path, &err);
+    if (!sc) g_err = "LoadScene: " + err;
+    return reinterpret_cast<pts_scene*>(sc);
+}
+
+int ptsSaveScene(pts_scene* s, const char* path)
+{
+    if (!s || !path) { g_err = "SaveScene: null argument"; return -1; }
+    std::string err;
+    if (!SaveScene(path, S(s), &err)) { g_err = "SaveScene: " + err; return -1; }
+    return 0;
+}
+
+uint32_t ptsSceneTextureCount(pts_scene* s) { return s ? (uint32_t)S(s)->Textures.size() : 0; }
+uint32_t ptsSceneMaterialCount(pts_scene* s) { return s ? (uint32_t)S(s)->Materials.size() : 0; }
+uint32_t ptsSceneMeshCount(pts_scene* s) { return s ? (uint32_t)S(s)->Meshes.size() : 0; }
+uint32_t ptsScenePrefabCount(pts_scene* s) { return s ? (uint32_t)S(s)->Prefabs.size() : 0; }
+
 pts_entity* ptsInstantiatePrefab(pts_scene* s, pts_prefab* p, pts_entity* parent)
 {
     return reinterpret_cast<pts_entity*>(

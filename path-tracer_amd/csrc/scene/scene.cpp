@@ -260,6 +260,7 @@ scene::~scene()
     for (material* M : Materials) delete M;
     for (texture* T : Textures) delete T;
     for (prefab* P : Prefabs) delete P;
+    if (OwnsSpectrumTable) delete RGBSpectrumTable;
 }
 
 scene* CreateEmptyScene()
@@ -555,7 +556,11 @@ uint32_t PackSceneData(scene* Scene)
             for (const mesh_face& F : Mesh->Faces) {
                 pt_packed_mesh_face P;
                 for (int j = 0; j < 3; j++) {
-                    vec3 Pos = Mesh->Vertices[F.VertexIndex[j]].Position;
+                    // A mesh loaded from a reference-written scene file has no
+                    // vertices (serializer.cpp): pack zero positions instead of
+                    // reading out of bounds; ptUpdateScene then rejects the faces.
+                    uint32_t Vi = F.VertexIndex[j];
+                    vec3 Pos = Vi < Mesh->Vertices.size() ? Mesh->Vertices[Vi].Position : vec3(0.0f);
                     float* Dst = j == 0 ? P.Position0 : (j == 1 ? P.Position1 : P.Position2);
                     Dst[0] = Pos.x; Dst[1] = Pos.y; Dst[2] = Pos.z;
                 }

@@ -52,6 +52,8 @@ struct texture {                      // scene.hpp:177-186
 struct material {                     // scene.hpp:188-196 + basic_*.hpp
     uint32_t Type = PT_MATERIAL_TYPE_BASIC_DIFFUSE;
     std::string Name = "New Material";
+    uint32_t Flags = 0;               // scene.hpp:192-193: editor data, serialised, not packed
+    float Opacity = 1.0f;
     uint32_t PackedMaterialIndex = 0;
 
     // basic_diffuse_material / basic_metal_material
@@ -175,6 +177,7 @@ struct scene {                        // scene.hpp:335-362
     std::vector<texture*> Textures;
     std::vector<prefab*> Prefabs;
     parametric_spectrum_table* RGBSpectrumTable = nullptr;
+    bool OwnsSpectrumTable = false;   // LoadScene read the scene's own spectrum.dat
 
     // Packed data (PackSceneData).
     uint32_t AtlasWidth = 4096, AtlasHeight = 4096;
@@ -216,6 +219,10 @@ texture* LoadTexture(scene* Scene, const char* Path, uint32_t Type, const char* 
 prefab* LoadModelAsPrefab(scene* Scene, const char* Path, const load_model_options* Options, std::string* Error);
 entity* CreateEntity(scene* Scene, const entity* Source, entity* Parent);
 entity* CreateEntity(scene* Scene, const prefab* Prefab, entity* Parent);
+
+// Scene file format (serializer.cpp; reference serializer.cpp:511-529).
+scene* LoadScene(const char* Path, std::string* Error);
+bool SaveScene(const char* Path, scene* Scene, std::string* Error);
 
 uint32_t PackSceneData(scene* Scene);
 void GetScenePacks(scene* Scene, pt_scene_packs* Out);

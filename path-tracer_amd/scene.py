@@ -51,6 +51,23 @@ class Scene:
         h = N.scene_lib().ptsCreateConfigScene(int(config_id), C.byref(info))
         return cls(h, info)
 
+    @classmethod
+    def load(cls, path):
+        """LoadScene (serializer.cpp:511-524): the scene JSON at `path` plus the
+        .texture / .mesh / spectrum.dat files beside it."""
+        return cls(N.scene_lib().ptsLoadScene(str(path).encode()))
+
+    def save(self, path):
+        """SaveScene (serializer.cpp:526-529)."""
+        if N.scene_lib().ptsSaveScene(self._h, str(path).encode()) != 0:
+            raise RuntimeError(N.scene_lib().ptsGetLastError().decode())
+
+    def counts(self):
+        """(textures, materials, meshes, prefabs) held by the scene."""
+        L = N.scene_lib()
+        return (L.ptsSceneTextureCount(self._h), L.ptsSceneMaterialCount(self._h), L.ptsSceneMeshCount(self._h),
+                L.ptsScenePrefabCount(self._h))
+
     def close(self):
         if self._h:
             N.scene_lib().ptsDestroyScene(self._h)
