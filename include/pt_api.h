@@ -212,6 +212,11 @@ int ptTraceRays(pt_device* device, pt_scene* scene, uint32_t n, const float* ori
  * returns the number of bit mismatches (must be 0). */
 int ptCheckFastDivision(pt_device* device, uint64_t n, uint32_t seed, uint64_t* mismatches);
 
+/* Diagnostic: evaluates the traversal's fast reciprocal (hardware rcp + one
+ * FMA Newton step) on every float d with 2^-126 <= |d| < 2^126 against the
+ * IEEE quotient 1.0f / d; returns the number of bit mismatches (must be 0). */
+int ptCheckFastReciprocal(pt_device* device, uint64_t* mismatches);
+
 /* Diagnostic: runs the extend step on the renderer's current rays with
  * traversal counters.  It writes the same hit records the next Run's extend
  * writes first, so the render is not perturbed.  out = {rays, lane steps, wave steps x 64, internal nodes,

@@ -237,6 +237,7 @@ HIP_API = {
     "ptReadPreviewImage": (_i32, [_vp, _vp, _fptr]),
     "ptReadPreviewAOVs": (_i32, [_vp, _vp, _vp]),
     "ptCheckFastDivision": (_i32, [_vp, C.c_uint64, _u32, C.POINTER(C.c_uint64)]),
+    "ptCheckFastReciprocal": (_i32, [_vp, C.POINTER(C.c_uint64)]),
     "ptExtendStats": (_i32, [_vp, _vp, C.POINTER(C.c_uint64)]),
     "ptSetProfiling": (_i32, [_vp, _i32]),
     "ptGetKernelStats": (_i32, [_vp, _i32, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
@@ -277,9 +278,12 @@ def hip_lib():
     """libpathtracer.so (HIP kernels for gfx950).  Raises if absent."""
     global _hip_lib
     if _hip_lib is None:
-        if not HIP_LIB_PATH.exists():
-            raise NativeLibraryMissing(f"{HIP_LIB_PATH} not built (run __graft_entry__.build())")
-        lib = C.CDLL(str(HIP_LIB_PATH))
+        # PT_HIP_LIB: an alternative build of the same library (compiler-flag
+        # experiments, tools/build_variant.py); the default is the in-tree one.
+        path = Path(os.environ.get("PT_HIP_LIB", str(HIP_LIB_PATH)))
+        if not path.exists():
+            raise NativeLibraryMissing(f"{path} not built (run __graft_entry__.build())")
+        lib = C.CDLL(str(path))
         _hip_lib = _bind(lib, HIP_API)
     return _hip_lib
 

@@ -54,14 +54,17 @@ def build_scene(force=False, verbose=True):
     return SCENE_LIB
 
 
-def build_hip(force=False, verbose=True):
-    if not force and not _stale(HIP_LIB, HIP_SRC + HIP_HDR + [Path(__file__)]):
-        return HIP_LIB
+def build_hip(force=False, verbose=True, out=None, extra=()):
+    out = Path(out) if out else HIP_LIB
+    if not force and not _stale(out, HIP_SRC + HIP_HDR + [Path(__file__)]):
+        return out
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-O3", "-fPIC", "-shared",
-           "-ffp-contract=off", "-fno-gpu-rdc", "-munsafe-fp-atomics",
-           "-Wno-unused-result", "-o", HIP_LIB] + HIP_SRC + [f"-L{ROCM}/lib", "-lrccl"]
+           # -fno-slp-vectorize: no v_pk_* f32 packing (and its operand moves);
+           # shade 0.164 -> 0.156 ms on C3, extend unchanged (tools/gpu_ab.sh).
+           "-ffp-contract=off", "-fno-gpu-rdc", "-munsafe-fp-atomics", "-fno-slp-vectorize",
+           "-Wno-unused-result", *extra, "-o", out] + HIP_SRC + [f"-L{ROCM}/lib", "-lrccl"]
     _run(cmd, verbose)
-    return HIP_LIB
+    return out
 
 
 def build_all(force=False, verbose=True):

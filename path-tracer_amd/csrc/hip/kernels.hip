@@ -741,6 +741,21 @@ __global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? 5 : 1) void shade_ke
     TileOrderStoreRay(L, s, valid, O, V, p16 >> 8);
 }
 
+// Exhaustive check of FastRcp: every bit pattern d = i (i < 2^32); counts
+// d in FastRcpRange whose FastRcp(d) differs from 1.0f / d in any bit.
+__global__ __launch_bounds__(256) void rcp_check_kernel(unsigned long long* mismatches)
+{
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint64_t stride = (uint64_t)gridDim.x * 256;
+    unsigned long long bad = 0;
+    for (; i < (1ull << 32); i += stride) {
+        float d = __uint_as_float((uint32_t)i);
+        if (!FastRcpRange(d)) continue;
+        bad += __float_as_uint(FastRcp(d)) != __float_as_uint(1.0f / d);
+    }
+    if (bad) atomicAdd(mismatches, bad);
+}
+
 // Checks XDiv against IEEE division on device-generated operands: counts
 // mismatching bit patterns (test infrastructure for the convention).
 __global__ __launch_bounds__(256) void xdiv_check_kernel(uint64_t n, uint32_t seed, unsigned long long* mismatches)
@@ -872,6 +887,12 @@ hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd
         hipLaunchKernelGGL(ptd::shade_kernel<PT_MATS_ALL>, dim3(Blocks(L.n)), dim3(256), 0, st, S, L, F, P);
         break;
     }
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_rcp_check(unsigned long long* mismatches, hipStream_t st)
+{
+    hipLaunchKernelGGL(ptd::rcp_check_kernel, dim3(8192), dim3(256), 0, st, mismatches);
     return hipGetLastError();
 }
 

@@ -70,6 +70,7 @@ hipError_t pt_launch_resolve(const float4* accum, uint32_t n, float brightness, 
                              uint32_t* out8, hipStream_t st);
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
                            uint32_t scene_mats, hipStream_t st);
+hipError_t pt_launch_rcp_check(unsigned long long* mismatches, hipStream_t st);
 hipError_t pt_launch_xdiv_check(uint64_t n, uint32_t seed, unsigned long long* mismatches, hipStream_t st);
 hipError_t pt_launch_trace_rays(const ptd::dscene& S, uint32_t n, const float* origins, const uint32_t* vel,
                                 const float* dur, float4* hit, float2* hc, float4* rec, float2* uv, uint32_t* spill,

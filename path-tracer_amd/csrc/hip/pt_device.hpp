@@ -176,6 +176,30 @@ PT_DEV float HwMax(float a, float b) { return __builtin_fmaxf(a, b); }
 PT_DEV float HwMin3(float a, float b, float c) { return __builtin_fminf(__builtin_fminf(a, b), c); }
 PT_DEV float HwMax3(float a, float b, float c) { return __builtin_fmaxf(__builtin_fmaxf(a, b), c); }
 
+// RN(1/d) from the hardware reciprocal (1 ulp) and one FMA Newton step.
+// Bit-identical to the IEEE quotient 1.0f / d for every float with
+// 2^-126 <= |d| < 2^126 (all 2^32 bit patterns checked on the device:
+// ptCheckFastReciprocal, tests/test_gpu_parity.py); callers keep IEEE
+// division outside that range.
+PT_DEV float FastRcp(float d)
+{
+    float y = __builtin_amdgcn_rcpf(d);
+    float e = __builtin_fmaf(-d, y, 1.0f);
+    return __builtin_fmaf(e, y, y);
+}
+
+// Traversal use (PT_FAST_RCP, traverse.hpp) is off: it measured 1 % slower
+// on C3 extend than the IEEE division sequence (tools/gpu_ab.sh).
+#ifndef PT_FAST_RCP
+#define PT_FAST_RCP 0
+#endif
+
+PT_DEV bool FastRcpRange(float d)
+{
+    float m = pt_abs(d);
+    return (m >= 0x1p-126f) & (m < 0x1p126f);
+}
+
 PT_DEV float FastQuot(float a, float b, float y)
 {
     float q = a * y;

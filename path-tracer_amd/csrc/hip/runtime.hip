@@ -912,6 +912,23 @@ int ptCheckFastDivision(pt_device* d, uint64_t n, uint32_t seed, uint64_t* misma
     return 0;
 }
 
+int ptCheckFastReciprocal(pt_device* d, uint64_t* mismatches)
+{
+    if (!d || !mismatches) { SetError("null argument"); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    unsigned long long* dm = nullptr;
+    PT_HIP(hipMalloc(&dm, sizeof(unsigned long long)));
+    hipError_t e = hipMemsetAsync(dm, 0, sizeof(unsigned long long), d->stream);
+    if (e == hipSuccess) e = pt_launch_rcp_check(dm, d->stream);
+    unsigned long long h = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&h, dm, sizeof(h), hipMemcpyDeviceToHost, d->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
+    (void)hipFree(dm);
+    if (e != hipSuccess) { SetError("ptCheckFastReciprocal: %s", hipGetErrorString(e)); return (int)e; }
+    *mismatches = h;
+    return 0;
+}
+
 int ptExtendStats(pt_device* d, pt_basic_renderer* r, uint64_t out[PT_EXTEND_STATS_COUNT])
 {
     if (!d || !out) { SetError("null argument"); return -1; }

@@ -54,7 +54,12 @@ PT_DEV void SetLevelRay(const dscene& S, lane_state& L, pt3 O, pt3 V)
     L.O = O;
     L.V = V;
     L.exact = S.fast_div && FastDivRay(O, V);
+#if PT_FAST_RCP
+    L.Y = v3(FastRcp(V.x), FastRcp(V.y), FastRcp(V.z));
+    if (!(FastRcpRange(V.x) & FastRcpRange(V.y) & FastRcpRange(V.z))) L.Y = v3(1.0f / V.x, 1.0f / V.y, 1.0f / V.z);
+#else
     L.Y = v3(1.0f / V.x, 1.0f / V.y, 1.0f / V.z);
+#endif
 }
 
 PT_DEV void LaneBegin(const dscene& S, lane_state& L, pt3 O, pt3 V, float Duration)
@@ -129,7 +134,13 @@ PT_DEV void LaneMeshFace(const dscene& S, uint32_t F, lane_state& L)
     pt3 RCE2 = cross(L.V, Edge2);
     float Det = dot(Edge1, RCE2);
     if (pt_abs(Det) < PT_EPSILON) return;
+#if PT_FAST_RCP
+    // FastRcp == 1.0f / Det bit for bit in its range (pt_device.hpp).
+    float InvDet = FastRcp(Det);
+    if (!FastRcpRange(Det)) InvDet = 1.0f / Det;
+#else
     float InvDet = 1.0f / Det;
+#endif
     pt3 Sv = L.O - P0;
     float U = InvDet * dot(Sv, RCE2);
     if (U < 0 || U > 1) return;

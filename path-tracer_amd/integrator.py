@@ -69,6 +69,11 @@ class Device:
         _check(N.hip_lib().ptCheckFastDivision(self._h, n, seed, C.byref(m)), "ptCheckFastDivision")
         return int(m.value)
 
+    def check_fast_reciprocal(self) -> int:
+        m = C.c_uint64(0)
+        _check(N.hip_lib().ptCheckFastReciprocal(self._h, C.byref(m)), "ptCheckFastReciprocal")
+        return int(m.value)
+
     def close(self):
         if self._h:
             N.hip_lib().ptDestroyDevice(self._h)

@@ -204,6 +204,12 @@ def test_fast_division_matches_ieee(pt, dev):
         assert dev.check_fast_division(1 << 28, seed) == 0
 
 
+def test_fast_reciprocal_matches_ieee_exhaustively(pt, dev):
+    """FastRcp (v_rcp_f32 + one FMA Newton step) equals 1.0f / d bit for bit
+    on all 2^32 inputs in its range 2^-126 <= |d| < 2^126."""
+    assert dev.check_fast_reciprocal() == 0
+
+
 def test_extend_stats_does_not_perturb(pt, dev):
     """ptExtendStats traces the current rays (as the next Run's extend would),
     so a render that calls it between rounds matches one that does not."""
