@@ -674,8 +674,11 @@ __global__ __launch_bounds__(256) void finalize_kernel(dscene S, uint32_t n, con
     uv[i] = make_float2(UV.x, UV.y);
 }
 
+#ifndef PT_SHADE_DIFFUSE_MINW
+#define PT_SHADE_DIFFUSE_MINW 5
+#endif
 template <uint32_t MATS>
-__global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? 5 : 1) void shade_kernel(dscene S, dslots L, dframe F,
+__global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MINW : 1) void shade_kernel(dscene S, dslots L, dframe F,
                                                                                     dparams Pm)
 {
     uint32_t s = blockIdx.x * 256 + threadIdx.x;   // one block per tile, no early exit (TileOrder)

@@ -276,21 +276,24 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
             float4 b0 = S.mesh_nodes[2 * Index + 2], b1 = S.mesh_nodes[2 * Index + 3];
             float TA = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, a0, a1, L.exact);
             float TB = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, b0, b1, L.exact);
-            if (TA > TB) {
-                if (TA < PT_INFINITY && L.dB < 32)
-                    st.put(L.dT + L.dB++, S.blas_words ? PackBlasEntry(__float_as_uint(a0.w), __float_as_uint(a1.w))
-                                                       : Index);
-                L.na = __float_as_uint(b0.w); L.nb = __float_as_uint(b1.w);
+            // The reference's three-way decision (scene.glsl.inc:366-392) as
+            // selects: B strictly closer -> continue with B, set A aside if
+            // hit; otherwise continue with A if hit, setting B aside if it
+            // was hit too; nothing hit -> pop.
+            bool goB = TA > TB;
+            bool any = goB | (TA < PT_INFINITY);
+            bool push = goB ? (TA < PT_INFINITY) : (TB < PT_INFINITY);
+            uint32_t aw0 = __float_as_uint(a0.w), aw1 = __float_as_uint(a1.w);
+            uint32_t bw0 = __float_as_uint(b0.w), bw1 = __float_as_uint(b1.w);
+            if (push & (L.dB < 32)) {
+                uint32_t e = S.blas_words ? PackBlasEntry(goB ? aw0 : bw0, goB ? aw1 : bw1) : Index + (goB ? 0u : 1u);
+                st.put(L.dT + L.dB++, e);
+            }
+            if (any) {
+                L.na = goB ? bw0 : aw0;
+                L.nb = goB ? bw1 : aw1;
                 return false;
             }
-            if (TB < PT_INFINITY) {
-                if (L.dB < 32)
-                    st.put(L.dT + L.dB++, S.blas_words ? PackBlasEntry(__float_as_uint(b0.w), __float_as_uint(b1.w))
-                                                       : Index + 1);
-                L.na = __float_as_uint(a0.w); L.nb = __float_as_uint(a1.w);
-                return false;
-            }
-            if (TA < PT_INFINITY) { L.na = __float_as_uint(a0.w); L.nb = __float_as_uint(a1.w); return false; }
         }
         if (L.dB > 0) {
             ss.pop();
@@ -341,17 +344,16 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
             float4 b0 = S.shape_nodes[2 * IB], b1 = S.shape_nodes[2 * IB + 1];
             float TA = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, a0, a1, L.exact);
             float TB = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, b0, b1, L.exact);
-            if (TA > TB) {
-                if (TA < PT_INFINITY && L.dT < 32) st.put(L.dT++, IA);
-                L.na = __float_as_uint(b0.w); L.nb = __float_as_uint(b1.w);
+            // Same decision as the BLAS step (scene.glsl.inc:494-516).
+            bool goB = TA > TB;
+            bool any = goB | (TA < PT_INFINITY);
+            bool push = goB ? (TA < PT_INFINITY) : (TB < PT_INFINITY);
+            if (push & (L.dT < 32)) st.put(L.dT++, goB ? IA : IB);
+            if (any) {
+                L.na = __float_as_uint(goB ? b0.w : a0.w);
+                L.nb = __float_as_uint(goB ? b1.w : a1.w);
                 return false;
             }
-            if (TB < PT_INFINITY) {
-                if (L.dT < 32) st.put(L.dT++, IB);
-                L.na = __float_as_uint(a0.w); L.nb = __float_as_uint(a1.w);
-                return false;
-            }
-            if (TA < PT_INFINITY) { L.na = __float_as_uint(a0.w); L.nb = __float_as_uint(a1.w); return false; }
         }
     }
     if (L.dT > 0) {
