@@ -131,9 +131,12 @@ PT_DEV void LaneMeshFace(const dscene& S, uint32_t F, lane_state& L)
     pt3 P0 = xyz(a);
     pt3 Edge1 = xyz(b);
     pt3 Edge2 = xyz(c);
+    // Every quantity is evaluated with the reference's operations and
+    // operand order; its early returns become one predicate (no value
+    // depends on which test failed first), so the exits collapse into a
+    // single select.
     pt3 RCE2 = cross(L.V, Edge2);
     float Det = dot(Edge1, RCE2);
-    if (pt_abs(Det) < PT_EPSILON) return;
 #if PT_FAST_RCP
     // FastRcp == 1.0f / Det bit for bit in its range (pt_device.hpp).
     float InvDet = FastRcp(Det);
@@ -143,12 +146,11 @@ PT_DEV void LaneMeshFace(const dscene& S, uint32_t F, lane_state& L)
 #endif
     pt3 Sv = L.O - P0;
     float U = InvDet * dot(Sv, RCE2);
-    if (U < 0 || U > 1) return;
     pt3 SCE1 = cross(Sv, Edge1);
     float W = InvDet * dot(L.V, SCE1);
-    if (W < 0 || U + W > 1) return;
     float T = InvDet * dot(Edge2, SCE1);
-    if (T < 0 || T > L.Time) return;
+    bool miss = (pt_abs(Det) < PT_EPSILON) | (U < 0) | (U > 1) | (W < 0) | (U + W > 1) | (T < 0) | (T > L.Time);
+    if (miss) return;
     L.Time = T;
     L.Shape = 0xFFFFFFFEu;
     L.Prim = F;
