@@ -223,6 +223,20 @@ PT_DEV float IntersectBoundingBox(pt3 O, pt3 V, pt3 Y, float Reach, float4 MinAn
     return SlabEntry(A / V, B / V, Reach);
 }
 
+// Both child boxes of an internal node under one `exact` branch (one
+// divergent branch per node instead of one per box).
+PT_DEV void IntersectBoxPair(pt3 O, pt3 V, pt3 Y, float Reach, float4 a0, float4 a1, float4 b0, float4 b1, bool exact,
+                             float& TA, float& TB)
+{
+    if (exact) {
+        TA = IntersectBoundingBox(O, V, Y, Reach, a0, a1, true);
+        TB = IntersectBoundingBox(O, V, Y, Reach, b0, b1, true);
+    } else {
+        TA = SlabEntry((xyz(a0) - O) / V, (xyz(a1) - O) / V, Reach);
+        TB = SlabEntry((xyz(b0) - O) / V, (xyz(b1) - O) / V, Reach);
+    }
+}
+
 struct rng {
     uint32_t State;
     PT_DEV float R01() { return pt_random01(&State); }

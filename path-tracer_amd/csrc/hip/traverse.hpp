@@ -245,71 +245,17 @@ struct complexity_stats {
 // box tests instead of the longest leaf's whole face loop.  The faces are
 // still tested in the reference's order, each with the Hit.Time left by the
 // previous one, and the pop follows the last face, so results are identical.
-template <bool SPILL, int CAP, class Src, class Stats = no_stats, bool FACE_STEP = false>
-PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, const Src& src, uint32_t slot,
-                     Stats& ss)
+// The TLAS-level part of a step (scene.glsl.inc:468-520) and the return from
+// a finished BLAS (scene.glsl.inc:409-411); rare on mesh scenes, so LaneStep
+// runs it as one block after the BLAS work instead of as early exits.
+template <bool SPILL, int CAP, class Src, class Stats>
+PT_DEV bool TlasStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, const Src& src, uint32_t slot, Stats& ss)
 {
-    ss.step();
     const uint32_t* mesh_words = reinterpret_cast<const uint32_t*>(S.mesh_nodes);
     const uint32_t* shape_words = reinterpret_cast<const uint32_t*>(S.shape_nodes);
     if (L.blas != SHAPE_INDEX_NONE) {
-        // IntersectMeshNode (scene.glsl.inc:336-399), one node.
-        if (L.nb > 0) {
-            if (FACE_STEP) {
-                if (L.na < L.nb) {
-                    LaneMeshFace(S, L.na, L);
-                    bool last = ++L.na == L.nb;
-                    ss.face_step(last);
-                    if (!last) return false;
-                } else {
-                    ss.face_step(true);
-                }
-            } else {
-                ss.node(true);
-                ss.leaf(L.nb - L.na);
-                for (uint32_t F = L.na; F < L.nb; F++) LaneMeshFace(S, F, L);
-            }
-        } else {
-            ss.node(true);
-            ss.internal();
-            uint32_t Index = L.na;
-            ss.coherence(Index);
-            float4 a0 = S.mesh_nodes[2 * Index], a1 = S.mesh_nodes[2 * Index + 1];
-            float4 b0 = S.mesh_nodes[2 * Index + 2], b1 = S.mesh_nodes[2 * Index + 3];
-            float TA = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, a0, a1, L.exact);
-            float TB = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, b0, b1, L.exact);
-            // The reference's three-way decision (scene.glsl.inc:366-392) as
-            // selects: B strictly closer -> continue with B, set A aside if
-            // hit; otherwise continue with A if hit, setting B aside if it
-            // was hit too; nothing hit -> pop.
-            bool goB = TA > TB;
-            bool any = goB | (TA < PT_INFINITY);
-            bool push = goB ? (TA < PT_INFINITY) : (TB < PT_INFINITY);
-            uint32_t aw0 = __float_as_uint(a0.w), aw1 = __float_as_uint(a1.w);
-            uint32_t bw0 = __float_as_uint(b0.w), bw1 = __float_as_uint(b1.w);
-            if (push & (L.dB < 32)) {
-                uint32_t e = S.blas_words ? PackBlasEntry(goB ? aw0 : bw0, goB ? aw1 : bw1) : Index + (goB ? 0u : 1u);
-                st.put(L.dT + L.dB++, e);
-            }
-            if (any) {
-                L.na = goB ? bw0 : aw0;
-                L.nb = goB ? bw1 : aw1;
-                return false;
-            }
-        }
-        if (L.dB > 0) {
-            ss.pop();
-            uint32_t E = st.get(L.dT + --L.dB);
-            if (S.blas_words) {
-                UnpackBlasEntry(E, L.na, L.nb);
-            } else {
-                L.na = mesh_words[8 * E + 3];
-                L.nb = mesh_words[8 * E + 7];
-            }
-            return false;
-        }
-        // IntersectMeshNode returned (scene.glsl.inc:409-411); back to the
-        // world-space ray for the rest of the shape traversal.
+        // IntersectMeshNode returned; back to the world-space ray for the
+        // rest of the shape traversal.
         if (L.Shape == 0xFFFFFFFEu) L.Shape = L.blas;
         L.blas = SHAPE_INDEX_NONE;
         if (L.dT == 0) return true;
@@ -318,7 +264,7 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
         src.load(slot, WO, WV, D);
         SetLevelRay(S, L, WO, WV);
     } else {
-        // Intersect (scene.glsl.inc:468-520), one node.
+        // Intersect, one node.
         ss.node(false);
         uint32_t Children = L.na;
         if (Children == 0) {
@@ -344,8 +290,8 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
             uint32_t IA = Children & 0xFFFF, IB = Children >> 16;
             float4 a0 = S.shape_nodes[2 * IA], a1 = S.shape_nodes[2 * IA + 1];
             float4 b0 = S.shape_nodes[2 * IB], b1 = S.shape_nodes[2 * IB + 1];
-            float TA = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, a0, a1, L.exact);
-            float TB = IntersectBoundingBox(L.O, L.V, L.Y, L.Time, b0, b1, L.exact);
+            float TA, TB;
+            IntersectBoxPair(L.O, L.V, L.Y, L.Time, a0, a1, b0, b1, L.exact, TA, TB);
             // Same decision as the BLAS step (scene.glsl.inc:494-516).
             bool goB = TA > TB;
             bool any = goB | (TA < PT_INFINITY);
@@ -366,6 +312,85 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
         return false;
     }
     return true;
+}
+
+// Advances one lane by one node.  Returns true when its Trace() is complete.
+// Only the two index words of the current node are carried between steps;
+// its bounds were already consumed by the parent's box test.
+//
+// FACE_STEP: a BLAS leaf advances by ONE face per step (na walks up to nb), so
+// a divergent wave step costs one face test beside the internal-node lanes'
+// box tests instead of the longest leaf's whole face loop.  The faces are
+// still tested in the reference's order, each with the Hit.Time left by the
+// previous one, and the pop follows the last face, so results are identical.
+//
+// The BLAS work (IntersectMeshNode, scene.glsl.inc:336-399) has no early
+// exit: it ends with the lane either moved to a new node, popped, or handed
+// to TlasStep (BLAS finished, or the lane is at the TLAS level).
+template <bool SPILL, int CAP, class Src, class Stats = no_stats, bool FACE_STEP = false>
+PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, const Src& src, uint32_t slot,
+                     Stats& ss)
+{
+    ss.step();
+    const uint32_t* mesh_words = reinterpret_cast<const uint32_t*>(S.mesh_nodes);
+    bool tlas = L.blas == SHAPE_INDEX_NONE;
+    if (!tlas) {
+        bool moved = false;
+        if (L.nb > 0) {
+            if (FACE_STEP) {
+                if (L.na < L.nb) LaneMeshFace(S, L.na, L);   // (an empty leaf tests nothing)
+                bool last = ++L.na >= L.nb;
+                ss.face_step(last);
+                moved = !last;
+            } else {
+                ss.node(true);
+                ss.leaf(L.nb - L.na);
+                for (uint32_t F = L.na; F < L.nb; F++) LaneMeshFace(S, F, L);
+            }
+        } else {
+            ss.node(true);
+            ss.internal();
+            uint32_t Index = L.na;
+            ss.coherence(Index);
+            float4 a0 = S.mesh_nodes[2 * Index], a1 = S.mesh_nodes[2 * Index + 1];
+            float4 b0 = S.mesh_nodes[2 * Index + 2], b1 = S.mesh_nodes[2 * Index + 3];
+            float TA, TB;
+            IntersectBoxPair(L.O, L.V, L.Y, L.Time, a0, a1, b0, b1, L.exact, TA, TB);
+            // The reference's three-way decision (scene.glsl.inc:366-392) as
+            // selects: B strictly closer -> continue with B, set A aside if
+            // hit; otherwise continue with A if hit, setting B aside if it
+            // was hit too; nothing hit -> pop.
+            bool goB = TA > TB;
+            moved = goB | (TA < PT_INFINITY);
+            bool push = goB ? (TA < PT_INFINITY) : (TB < PT_INFINITY);
+            uint32_t aw0 = __float_as_uint(a0.w), aw1 = __float_as_uint(a1.w);
+            uint32_t bw0 = __float_as_uint(b0.w), bw1 = __float_as_uint(b1.w);
+            if (push & (L.dB < 32)) {
+                uint32_t e = S.blas_words ? PackBlasEntry(goB ? aw0 : bw0, goB ? aw1 : bw1) : Index + (goB ? 0u : 1u);
+                st.put(L.dT + L.dB++, e);
+            }
+            if (moved) {
+                L.na = goB ? bw0 : aw0;
+                L.nb = goB ? bw1 : aw1;
+            }
+        }
+        if (!moved) {
+            if (L.dB > 0) {
+                ss.pop();
+                uint32_t E = st.get(L.dT + --L.dB);
+                if (S.blas_words) {
+                    UnpackBlasEntry(E, L.na, L.nb);
+                } else {
+                    L.na = mesh_words[8 * E + 3];
+                    L.nb = mesh_words[8 * E + 7];
+                }
+            } else {
+                tlas = true;
+            }
+        }
+    }
+    if (!tlas) return false;
+    return TlasStep(S, L, st, src, slot, ss);
 }
 
 // Hit attribute reconstruction (scene.glsl.inc:535-608).
