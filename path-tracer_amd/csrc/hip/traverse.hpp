@@ -125,9 +125,12 @@ PT_DEV void IntersectAnalytic(int32_t Type, pt3 O, pt3 V, uint32_t ShapeIndex, l
 // the edges are the reference's `Position1 - Position0`, `Position2 -
 // Position0`, subtracted once on the host at upload in the same IEEE
 // arithmetic, so every later operation sees identical operands.
-PT_DEV void LaneMeshFace(const dscene& S, uint32_t F, lane_state& L)
+PT_DEV void LaneMeshFace(const dscene& S, uint32_t F, lane_state& L, bool valid = true)
 {
-    float4 a = S.mesh_faces[3 * F + 0], b = S.mesh_faces[3 * F + 1], c = S.mesh_faces[3 * F + 2];
+    // valid == false (an empty leaf): face 0 is read and the test forced to
+    // miss, instead of a branch around the call.
+    uint32_t Fl = valid ? F : 0u;
+    float4 a = S.mesh_faces[3 * Fl + 0], b = S.mesh_faces[3 * Fl + 1], c = S.mesh_faces[3 * Fl + 2];
     pt3 P0 = xyz(a);
     pt3 Edge1 = xyz(b);
     pt3 Edge2 = xyz(c);
@@ -149,12 +152,13 @@ PT_DEV void LaneMeshFace(const dscene& S, uint32_t F, lane_state& L)
     pt3 SCE1 = cross(Sv, Edge1);
     float W = InvDet * dot(L.V, SCE1);
     float T = InvDet * dot(Edge2, SCE1);
-    bool miss = (pt_abs(Det) < PT_EPSILON) | (U < 0) | (U > 1) | (W < 0) | (U + W > 1) | (T < 0) | (T > L.Time);
-    if (miss) return;
-    L.Time = T;
-    L.Shape = 0xFFFFFFFEu;
-    L.Prim = F;
-    L.C = v3(1 - U - W, U, W);
+    bool miss = (pt_abs(Det) < PT_EPSILON) | (U < 0) | (U > 1) | (W < 0) | (U + W > 1) | (T < 0) | (T > L.Time) | !valid;
+    // Selects, not a branch: the hit registers are updated in place (a
+    // conditional update made the compiler keep and copy a second set).
+    L.Time = miss ? L.Time : T;
+    L.Shape = miss ? L.Shape : 0xFFFFFFFEu;
+    L.Prim = miss ? L.Prim : F;
+    L.C = v3(miss ? L.C.x : 1 - U - W, miss ? L.C.y : U, miss ? L.C.z : W);
 }
 
 // Traversal statistics hooks: no-ops in the render kernel, counters in the
@@ -338,7 +342,7 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
         bool moved = false;
         if (L.nb > 0) {
             if (FACE_STEP) {
-                if (L.na < L.nb) LaneMeshFace(S, L.na, L);   // (an empty leaf tests nothing)
+                LaneMeshFace(S, L.na, L, L.na < L.nb);   // (an empty leaf tests nothing)
                 bool last = ++L.na >= L.nb;
                 ss.face_step(last);
                 moved = !last;
