@@ -84,15 +84,16 @@ PT_HD float pt_rint(float x)
 /* --- exp / log --------------------------------------------------------------- */
 
 /* e^x.  Cody–Waite reduction x = k ln2 + r, |r| <= ln2/2, degree-7 Taylor
- * polynomial in Horner form, then exact scaling by 2^k (two steps for the
- * subnormal range). */
+ * polynomial in Horner form, then exact scaling by 2^k in two steps
+ * 2^k1 * 2^(k - k1) with k1 = clamp(k, -126, 127) (k - k1 = 0 in the normal
+ * range, where the second factor is exactly 1; the subnormal and overflow
+ * ranges need both).  Branch-free: the out-of-range and NaN inputs are
+ * resolved by selects after the common path, on a clamped argument. */
 PT_HD float pt_exp(float x)
 {
-    if (!(x == x)) return x;                       /* NaN */
-    if (x > 88.72283935546875f) return pt_u2f(0x7f800000u);
-    if (x < -103.97208404541015625f) return 0.0f;
-    float k = pt_rint(x * 1.44269502162933349609375f);
-    float r = (x - k * 0.693145751953125f) - k * 1.428606765330187045e-06f;
+    float xc = pt_min(pt_max(x, -103.97208404541015625f), 88.72283935546875f);
+    float k = pt_rint(xc * 1.44269502162933349609375f);
+    float r = (xc - k * 0.693145751953125f) - k * 1.428606765330187045e-06f;
     float p = 1.98412698412698413e-04f;            /* 1/5040 */
     p = p * r + 1.38888888888888889e-03f;          /* 1/720 */
     p = p * r + 8.33333333333333333e-03f;          /* 1/120 */
@@ -102,9 +103,11 @@ PT_HD float pt_exp(float x)
     p = p * r + 1.0f;
     p = p * r + 1.0f;
     int ki = (int)k;
-    if (ki > 127) { return p * pt_pow2i(127) * pt_pow2i(ki - 127); }
-    if (ki < -126) { return p * pt_pow2i(-126) * pt_pow2i(ki + 126); }
-    return p * pt_pow2i(ki);
+    int k1 = ki < -126 ? -126 : (ki > 127 ? 127 : ki);
+    float y = p * pt_pow2i(k1) * pt_pow2i(ki - k1);
+    y = x > 88.72283935546875f ? pt_u2f(0x7f800000u) : y;
+    y = x < -103.97208404541015625f ? 0.0f : y;
+    return x == x ? y : x;                         /* NaN */
 }
 
 /* Natural logarithm (fdlibm e_logf.c structure: x = 2^e (1+f),
@@ -171,28 +174,23 @@ PT_HD float pt_cos_kernel(float r)
     return y + 1.0f;
 }
 
+/* Quadrant selection by selects (both kernels are evaluated). */
 PT_HD float pt_sin(float x)
 {
     int q;
     float r = pt_reduce_pio2(x, &q);
-    switch (q & 3) {
-        case 0: return pt_sin_kernel(r);
-        case 1: return pt_cos_kernel(r);
-        case 2: return -pt_sin_kernel(r);
-        default: return -pt_cos_kernel(r);
-    }
+    float s = pt_sin_kernel(r), c = pt_cos_kernel(r);
+    float v = (q & 1) ? c : s;
+    return (q & 2) ? -v : v;
 }
 
 PT_HD float pt_cos(float x)
 {
     int q;
     float r = pt_reduce_pio2(x, &q);
-    switch (q & 3) {
-        case 0: return pt_cos_kernel(r);
-        case 1: return -pt_sin_kernel(r);
-        case 2: return -pt_cos_kernel(r);
-        default: return pt_sin_kernel(r);
-    }
+    float s = pt_sin_kernel(r), c = pt_cos_kernel(r);
+    float v = (q & 1) ? s : c;
+    return ((q + 1) & 2) ? -v : v;
 }
 
 /* --- atan2 / asin ------------------------------------------------------------ */

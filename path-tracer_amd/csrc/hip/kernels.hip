@@ -442,8 +442,14 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
             pt4 Emission = SampleSkyboxRadiance(S, V, Lambda);
             float ClusterPDF = Path.Probability.x + Path.Probability.y + Path.Probability.z + Path.Probability.w;
             pt4 E = Emission * Path.Throughput;
-            pt3 XYZ = SampleStandardObserver(Lambda.x) * E.x + SampleStandardObserver(Lambda.y) * E.y +
-                      SampleStandardObserver(Lambda.z) * E.z + SampleStandardObserver(Lambda.w) * E.w;
+            // Left-to-right sum over the four wavelengths (the reference's
+            // expression order) as a rolled loop: one observer evaluation's
+            // registers at a time.
+            float Lv[4] = {Lambda.x, Lambda.y, Lambda.z, Lambda.w};
+            float Ev[4] = {E.x, E.y, E.z, E.w};
+            pt3 XYZ = SampleStandardObserver(Lv[0]) * Ev[0];
+#pragma unroll 1
+            for (int I = 1; I < 4; I++) XYZ = XYZ + SampleStandardObserver(Lv[I]) * Ev[I];
             Path.Sample = Path.Sample + XYZ / ClusterPDF;
             Path.Probability = v4s(0.0f);
         }
