@@ -735,7 +735,13 @@ __global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MIN
         }
 
         if (Scatter<MATS>(S, G, Pm.termination_probability, P, O, V, HitShape, HitMaterial, HitTime, PN, PTg, UV)) {
-            StorePathVertex(L, s, P);
+            // StorePathVertex of a continuing path: Scatter changes Sample only
+            // on escape (which terminates the path) and never Lambda0, so smp
+            // is unchanged; the active-shape stack is written when it moved.
+            L.thr[s] = make_float4(P.Throughput.x, P.Throughput.y, P.Throughput.z, P.Throughput.w);
+            L.prob[s] = make_float4(P.Probability.x, P.Probability.y, P.Probability.z, P.Probability.w);
+            uint2 na = make_uint2((P.Active[1] << 16) | P.Active[0], (P.Active[3] << 16) | P.Active[2]);
+            if ((na.x != act.x) | (na.y != act.y)) L.act[s] = na;
         } else {
             float4* A = &F.accum[(size_t)y * F.width + x];
             float4 Val = make_float4(P.Sample.x, P.Sample.y, P.Sample.z, 1.0f);
