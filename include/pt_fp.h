@@ -70,6 +70,16 @@ PT_HD float pt_sign(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f
 PT_HD float pt_mix(float x, float y, float a) { return x * (1.0f - a) + y * a; }
 PT_HD uint32_t pt_umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
+/* Fused multiply-add, correctly rounded on both sides (v_fma_f32 on the
+ * device, C99 fmaf on the host): the polynomial kernels below evaluate
+ * their Horner steps with it (one rounding per step, half the operations).
+ * Written out explicitly, so -ffp-contract=off still governs everything else. */
+#ifdef __HIP_DEVICE_COMPILE__
+PT_HD float pt_fma(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+#else
+PT_HD float pt_fma(float a, float b, float c) { return fmaf(a, b, c); }
+#endif
+
 /* 2^k for integer k in [-126, 127] by exponent construction (exact). */
 PT_HD float pt_pow2i(int k) { return pt_u2f((uint32_t)(k + 127) << 23); }
 
@@ -95,13 +105,13 @@ PT_HD float pt_exp(float x)
     float k = pt_rint(xc * 1.44269502162933349609375f);
     float r = (xc - k * 0.693145751953125f) - k * 1.428606765330187045e-06f;
     float p = 1.98412698412698413e-04f;            /* 1/5040 */
-    p = p * r + 1.38888888888888889e-03f;          /* 1/720 */
-    p = p * r + 8.33333333333333333e-03f;          /* 1/120 */
-    p = p * r + 4.16666666666666667e-02f;          /* 1/24 */
-    p = p * r + 1.66666666666666667e-01f;          /* 1/6 */
-    p = p * r + 0.5f;
-    p = p * r + 1.0f;
-    p = p * r + 1.0f;
+    p = pt_fma(p, r, 1.38888888888888889e-03f);          /* 1/720 */
+    p = pt_fma(p, r, 8.33333333333333333e-03f);          /* 1/120 */
+    p = pt_fma(p, r, 4.16666666666666667e-02f);          /* 1/24 */
+    p = pt_fma(p, r, 1.66666666666666667e-01f);          /* 1/6 */
+    p = pt_fma(p, r, 0.5f);
+    p = pt_fma(p, r, 1.0f);
+    p = pt_fma(p, r, 1.0f);
     int ki = (int)k;
     int k1 = ki < -126 ? -126 : (ki > 127 ? 127 : ki);
     float y = p * pt_pow2i(k1) * pt_pow2i(ki - k1);
@@ -131,8 +141,8 @@ PT_HD float pt_log(float x)
     float s = f / (2.0f + f);
     float z = s * s;
     float w = z * z;
-    float t1 = w * (4.0000000596e-01f + w * 2.2222198546e-01f);
-    float t2 = z * (6.6666668653e-01f + w * 2.8571429849e-01f);
+    float t1 = w * pt_fma(w, 2.2222198546e-01f, 4.0000000596e-01f);
+    float t2 = z * pt_fma(w, 2.8571429849e-01f, 6.6666668653e-01f);
     float R = t2 + t1;
     float hfsq = 0.5f * f * f;
     float dk = (float)e;
@@ -158,19 +168,19 @@ PT_HD float pt_sin_kernel(float r)
 {
     float z = r * r;
     float p = -1.9515295891e-4f;
-    p = p * z + 8.3321608736e-3f;
-    p = p * z + -1.6666654611e-1f;
-    return p * z * r + r;
+    p = pt_fma(p, z, 8.3321608736e-3f);
+    p = pt_fma(p, z, -1.6666654611e-1f);
+    return pt_fma(p * z, r, r);
 }
 
 PT_HD float pt_cos_kernel(float r)
 {
     float z = r * r;
     float p = 2.443315711809948e-5f;
-    p = p * z + -1.388731625493765e-3f;
-    p = p * z + 4.166664568298827e-2f;
+    p = pt_fma(p, z, -1.388731625493765e-3f);
+    p = pt_fma(p, z, 4.166664568298827e-2f);
     float y = p * z * z;
-    y = y - 0.5f * z;
+    y = pt_fma(-0.5f, z, y);
     return y + 1.0f;
 }
 
@@ -203,10 +213,10 @@ PT_HD float pt_atan_pos(float t)
     else if (t > 0.4142135623730950f) { y0 = 0.7853981633974483f; t = (t - 1.0f) / (t + 1.0f); }
     float z = t * t;
     float p = 8.05374449538e-2f;
-    p = p * z + -1.38776856032e-1f;
-    p = p * z + 1.99777106478e-1f;
-    p = p * z + -3.33329491539e-1f;
-    return y0 + (p * z * t + t);
+    p = pt_fma(p, z, -1.38776856032e-1f);
+    p = pt_fma(p, z, 1.99777106478e-1f);
+    p = pt_fma(p, z, -3.33329491539e-1f);
+    return y0 + pt_fma(p * z, t, t);
 }
 
 /* GLSL atan(y, x); returns 0 for (0, 0). */
@@ -230,11 +240,11 @@ PT_HD float pt_asin(float x)
     if (a > 0.5f) { z = 0.5f * (1.0f - a); s = pt_sqrt(z); flag = 1.0f; }
     else { z = a * a; s = a; }
     float p = 4.2163199048e-2f;
-    p = p * z + 2.4181311049e-2f;
-    p = p * z + 4.5470025998e-2f;
-    p = p * z + 7.4953002686e-2f;
-    p = p * z + 1.6666752422e-1f;
-    float r = p * z * s + s;
+    p = pt_fma(p, z, 2.4181311049e-2f);
+    p = pt_fma(p, z, 4.5470025998e-2f);
+    p = pt_fma(p, z, 7.4953002686e-2f);
+    p = pt_fma(p, z, 1.6666752422e-1f);
+    float r = pt_fma(p * z, s, s);
     if (flag != 0.0f) r = 1.5707963267948966f - (r + r);
     return x < 0.0f ? -r : r;
 }
