@@ -56,6 +56,16 @@ def measured_traffic(kernel):
     return k.get("hbm_bytes"), d.get("profile")
 
 
+def measured_issue(kernel):
+    """VALU issue utilisation of `kernel` from the committed PMC profile
+    (profiles/traffic.json "issue"): the bound that actually limits the
+    traversal and shading kernels, which are far below the HBM roofline."""
+    p = ROOT / "profiles" / "traffic.json"
+    if not p.exists():
+        return None
+    return json.loads(p.read_text()).get("issue", {}).get(kernel)
+
+
 def cpu_baseline(pt, scene, width, height, max_seconds=12.0, max_rounds=200):
     """Time the CPU oracle (scalar C++ restatement, std::thread over host
     cores) on the same scene and frame.  Bounded: Reset + Run(2) warm-up, then
@@ -251,6 +261,11 @@ def main():
             "launch_avg_ms": {"extend": round(avg_ext, 4), "shade": round(avg_sh, 4)},
             "path_gbps_220B_per_ray": round(PATH_BYTES_PER_RAY * rays / dt / 1e9, 2),
         },
+        # What bounds the dominant kernel instead of HBM (PMC, same profile):
+        # fraction of the chip's VALU issue slots used, and active lanes per
+        # VALU instruction (of 64; divergence).
+        "limiter": {"kind": "valu_issue", "kernel": dom, **(measured_issue(dom) or {}),
+                    "source": traffic_src},
     }
     # Node/face bytes the traversal pulls through L1/L2 per ray (BVH + faces
     # are cache-resident): internal node = both child boxes (64 B), face 48 B,
