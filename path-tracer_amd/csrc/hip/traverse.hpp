@@ -130,7 +130,8 @@ PT_DEV void LaneMeshFace(const dscene& S, uint32_t F, lane_state& L, bool valid 
     // valid == false (an empty leaf): face 0 is read and the test forced to
     // miss, instead of a branch around the call.
     uint32_t Fl = valid ? F : 0u;
-    float4 a = S.mesh_faces[3 * Fl + 0], b = S.mesh_faces[3 * Fl + 1], c = S.mesh_faces[3 * Fl + 2];
+    const float4* Fp = S.mesh_faces + 3 * (size_t)Fl;   // one address, immediate offsets
+    float4 a = Fp[0], b = Fp[1], c = Fp[2];
     pt3 P0 = xyz(a);
     pt3 Edge1 = xyz(b);
     pt3 Edge2 = xyz(c);
@@ -292,8 +293,9 @@ PT_DEV bool TlasStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
         } else {
             ss.internal();
             uint32_t IA = Children & 0xFFFF, IB = Children >> 16;
-            float4 a0 = S.shape_nodes[2 * IA], a1 = S.shape_nodes[2 * IA + 1];
-            float4 b0 = S.shape_nodes[2 * IB], b1 = S.shape_nodes[2 * IB + 1];
+            const float4* Ap = S.shape_nodes + 2 * (size_t)IA;
+            const float4* Bp = S.shape_nodes + 2 * (size_t)IB;
+            float4 a0 = Ap[0], a1 = Ap[1], b0 = Bp[0], b1 = Bp[1];
             float TA, TB;
             IntersectBoxPair(L.O, L.V, L.Y, L.Time, a0, a1, b0, b1, L.exact, TA, TB);
             // Same decision as the BLAS step (scene.glsl.inc:494-516).
@@ -356,8 +358,8 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
             ss.internal();
             uint32_t Index = L.na;
             ss.coherence(Index);
-            float4 a0 = S.mesh_nodes[2 * Index], a1 = S.mesh_nodes[2 * Index + 1];
-            float4 b0 = S.mesh_nodes[2 * Index + 2], b1 = S.mesh_nodes[2 * Index + 3];
+            const float4* Np = S.mesh_nodes + 2 * (size_t)Index;   // child pair: 64 contiguous bytes
+            float4 a0 = Np[0], a1 = Np[1], b0 = Np[2], b1 = Np[3];
             float TA, TB;
             IntersectBoxPair(L.O, L.V, L.Y, L.Time, a0, a1, b0, b1, L.exact, TA, TB);
             // The reference's three-way decision (scene.glsl.inc:366-392) as
