@@ -471,7 +471,7 @@ PT_DEV pt4 SampleSkyboxRadiance(const dscene& S, pt3 D, pt4 Lambda)
     return (Spectrum.w * SampleParametricSpectrum(v3(Spectrum.x, Spectrum.y, Spectrum.z), Lambda)) * S.g.SkyboxBrightness;
 }
 
-PT_DEV uint32_t MUint(const dscene& S, uint32_t M, uint32_t A) { return S.material[32 * M + A]; }
+PT_DEV uint32_t MUint(const dscene& S, uint32_t M, uint32_t A) { return S.material[32 * (size_t)M + A]; }
 PT_DEV float MFloat(const dscene& S, uint32_t M, uint32_t A) { return pt_u2f(MUint(S, M, A)); }
 PT_DEV pt3 MVec3(const dscene& S, uint32_t M, uint32_t A) { return v3(MFloat(S, M, A), MFloat(S, M, A + 1), MFloat(S, M, A + 2)); }
 

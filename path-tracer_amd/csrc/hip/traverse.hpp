@@ -409,9 +409,8 @@ PT_DEV void HitAttributes(const dscene& S, uint32_t ShapeIndex, uint32_t Prim, p
     const float* To = Shape->Transform.To;
     const float* From = Shape->Transform.From;
     if (Type == PT_SHAPE_TYPE_MESH_INSTANCE) {
-        float4 f0 = S.mesh_faces[3 * Prim + 0];
-        float4 f1 = S.mesh_faces[3 * Prim + 1];
-        float4 f2 = S.mesh_faces[3 * Prim + 2];
+        const float4* Fp = S.mesh_faces + 3 * (size_t)Prim;
+        float4 f0 = Fp[0], f1 = Fp[1], f2 = Fp[2];
         uint2 V0 = S.mesh_vertices[__float_as_uint(f0.w)];
         uint2 V1 = S.mesh_vertices[__float_as_uint(f1.w)];
         uint2 V2 = S.mesh_vertices[__float_as_uint(f2.w)];
