@@ -319,6 +319,43 @@ PT_DEV void StorePathVertex(const dslots& L, uint32_t s, const path& P)
     L.act[s] = make_uint2((P.Active[1] << 16) | P.Active[0], (P.Active[3] << 16) | P.Active[2]);
 }
 
+// Position of the k-th set bit (k < popcount) of a 64-bit word: a 6-step
+// binary search over popcounts of the low halves.
+PT_DEV uint32_t SelectBit64(uint64_t m, uint32_t k)
+{
+    uint32_t pos = 0;
+    uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+    uint32_t c = (uint32_t)__popc(lo);
+    uint32_t w = lo;
+    if (k >= c) { k -= c; w = hi; pos = 32; }
+#pragma unroll
+    for (uint32_t width = 16; width >= 1; width >>= 1) {
+        uint32_t cw = (uint32_t)__popc(w & ((1u << width) - 1u));
+        if (k >= cw) { k -= cw; w >>= width; pos += width; }
+    }
+    return pos;
+}
+
+// ShadeOrder: the position shaded by thread u of a tile, hits (and positions
+// outside the image) first in position order, then misses, from the tile's
+// miss mask (extend).  Tile-uniform mask words, no barrier.
+PT_DEV uint32_t ShadePosition(const uint64_t* mask, uint32_t u)
+{
+    uint64_t m0 = mask[0], m1 = mask[1], m2 = mask[2], m3 = mask[3];
+    uint32_t c0 = (uint32_t)__popcll(~m0), c1 = (uint32_t)__popcll(~m1), c2 = (uint32_t)__popcll(~m2);
+    uint32_t nhit = c0 + c1 + c2 + (uint32_t)__popcll(~m3);
+    bool hit = u < nhit;
+    uint32_t k = hit ? u : u - nhit;
+    uint64_t w0 = hit ? ~m0 : m0, w1 = hit ? ~m1 : m1, w2 = hit ? ~m2 : m2, w3 = hit ? ~m3 : m3;
+    uint32_t n0 = hit ? c0 : 64u - c0, n1 = hit ? c1 : 64u - c1, n2 = hit ? c2 : 64u - c2;
+    uint32_t word = 0;
+    uint64_t w = w0;
+    if (k >= n0) { k -= n0; word = 1; w = w1;
+        if (k >= n1) { k -= n1; word = 2; w = w2;
+            if (k >= n2) { k -= n2; word = 3; w = w3; } } }
+    return word * 64 + SelectBit64(w, k);
+}
+
 // TileOrder: called by all 256 threads of a block (one tile) once their new
 // rays are known.  Sort key: direction octant (0-7) for valid slots, 8 for
 // slots outside the image.  Per wave, a ballot per key gives each lane its
@@ -352,6 +389,7 @@ PT_DEV void TileOrderStoreRay(const dslots& L, uint32_t s, bool valid, pt3 O, pt
     uint32_t q = (s & ~255u) | p;
     L.ray[q] = make_float4(O.x, O.y, O.z, __uint_as_float(PackUnitVector(V)));
     L.pos[s] = (uint16_t)((p << 8) | hitbyte);
+    L.slotof[q] = (uint8_t)(s & 255u);
 }
 
 // GenerateNewPath (basic_scatter.glsl:7-42) + GenerateCameraRay (scene.glsl.inc:613-655)
@@ -526,6 +564,10 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
 
 // One block per tile (the slot count is a multiple of 256): TileOrder needs
 // every thread of the block, so no thread returns early.
+#ifndef PT_SHADE_ORDER
+#define PT_SHADE_ORDER 1
+#endif
+
 __global__ __launch_bounds__(256) void raygen_kernel(dscene S, dslots L, dframe F, dparams Pm)
 {
     uint32_t s = blockIdx.x * 256 + threadIdx.x;
@@ -561,9 +603,16 @@ struct ray_source_slots {
         L.hit[s] = make_float4(Ln.Time, __uint_as_float(Ln.Shape), __uint_as_float(Ln.Prim), Ln.C.x);
         L.uv[s] = make_float2(Ln.C.y, Ln.C.z);
     }
+    // ShadeOrder: each wave, once all its rays are traced, stores the ballot
+    // of its escaped rays (one word per 64 positions; no atomics, no barrier).
+    PT_DEV void outcome(uint32_t q, uint64_t miss_ballot) const
+    {
+        if ((q & 63u) == 0) L.missmask[q >> 6] = miss_ballot;
+    }
 };
 
 struct ray_source_arrays {
+    PT_DEV void outcome(uint32_t, uint64_t) const {}
     const float* origins;
     const uint32_t* vel;
     const float* dur;
@@ -599,13 +648,17 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
     st.stride = spill_stride;
     pt3 O, V;
     float D;
-    if (!src.load(slot, O, V, D)) return;
-    lane_state Ln;
-    LaneBegin(S, Ln, O, V, D);
-    no_stats ns;
-    if (S.g.ShapeCount != 0)
-        while (!LaneStep<SPILL, CAP, Src, no_stats, true>(S, Ln, st, src, slot, ns)) {}
-    src.store(slot, Ln);
+    bool miss = false;
+    if (src.load(slot, O, V, D)) {
+        lane_state Ln;
+        LaneBegin(S, Ln, O, V, D);
+        no_stats ns;
+        if (S.g.ShapeCount != 0)
+            while (!LaneStep<SPILL, CAP, Src, no_stats, true>(S, Ln, st, src, slot, ns)) {}
+        src.store(slot, Ln);
+        miss = Ln.Shape == SHAPE_INDEX_NONE;
+    }
+    src.outcome(slot, __ballot(miss));
 }
 
 PT_DEV uint32_t WaveSum(uint32_t v)
@@ -687,7 +740,16 @@ template <uint32_t MATS>
 __global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MINW : 1) void shade_kernel(dscene S, dslots L, dframe F,
                                                                                     dparams Pm)
 {
-    uint32_t s = blockIdx.x * 256 + threadIdx.x;   // one block per tile, no early exit (TileOrder)
+    // One block per tile, no early exit (TileOrder).  ShadeOrder: thread u
+    // shades the slot whose ray sits at ShadePosition(u), so the waves of a
+    // tile run the surface path or the escape path, mostly not both; path
+    // state is read and written by slot (gathers within the tile's records).
+    const uint32_t base = blockIdx.x * 256;
+#if PT_SHADE_ORDER
+    uint32_t s = base | L.slotof[base | ShadePosition(L.missmask + 4 * (size_t)blockIdx.x, threadIdx.x)];
+#else
+    uint32_t s = base | threadIdx.x;
+#endif
     uint32_t x, y;
     bool valid = SlotPixel(F, s, x, y);
     uint32_t p16 = L.pos[s];

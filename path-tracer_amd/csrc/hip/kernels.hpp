@@ -28,6 +28,8 @@ struct dslots {
     uint2* act;         // active-shape stack (2 x u16 pairs)
     uint16_t* pos;      // per slot: position of its current ray (high byte) and of
                         // its last traced hit (low byte) within its tile (TileOrder)
+    uint8_t* slotof;    // per position: the slot (within the tile) whose ray sits there
+    uint64_t* missmask; // per tile, 4 words: bit t set iff the ray at position t escaped (by extend)
     uint32_t* spill;    // traversal stack spill: (needed - LDS capacity) rows x n
     uint32_t n;
 };

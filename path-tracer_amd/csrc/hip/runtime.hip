@@ -136,6 +136,8 @@ struct pt_basic_renderer {
     dbuf<float2> uv;
     dbuf<uint2> act;
     dbuf<uint16_t> pos;                 // TileOrder positions (kernels.hip)
+    dbuf<uint8_t> slotof;               // position -> slot within the tile
+    dbuf<uint64_t> missmask;            // ShadeOrder: escaped-ray bits per tile (extend -> shade)
     dbuf<uint32_t> spill;
 };
 
@@ -624,17 +626,25 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     uint32_t ns = (uint32_t)n;
     bool ok = r->ray.alloc(ns) == hipSuccess && r->hit.alloc(ns) == hipSuccess && r->thr.alloc(ns) == hipSuccess &&
               r->prob.alloc(ns) == hipSuccess && r->smp.alloc(ns) == hipSuccess && r->uv.alloc(ns) == hipSuccess &&
-              r->act.alloc(ns) == hipSuccess && r->pos.alloc(ns) == hipSuccess;
+              r->act.alloc(ns) == hipSuccess && r->pos.alloc(ns) == hipSuccess && r->slotof.alloc(ns) == hipSuccess &&
+              r->missmask.alloc(ns / 64 + 1) == hipSuccess;
     if (ok && ns) {
         ok = hipMemset(r->ray.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->hit.ptr, 0, (size_t)ns * 16) == hipSuccess &&
              hipMemset(r->thr.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->prob.ptr, 0, (size_t)ns * 16) == hipSuccess &&
              hipMemset(r->smp.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->uv.ptr, 0, (size_t)ns * 8) == hipSuccess &&
-             hipMemset(r->act.ptr, 0, (size_t)ns * 8) == hipSuccess && hipMemset(r->pos.ptr, 0, (size_t)ns * 2) == hipSuccess;
+             hipMemset(r->act.ptr, 0, (size_t)ns * 8) == hipSuccess &&
+             hipMemset(r->missmask.ptr, 0, (size_t)(ns / 64 + 1) * 8) == hipSuccess;
+        // Identity TileOrder until the first Reset sorts the rays.
+        std::vector<uint16_t> pos(ns);
+        std::vector<uint8_t> slotof(ns);
+        for (uint32_t i = 0; i < ns; i++) { pos[i] = (uint16_t)(((i & 255u) << 8) | (i & 255u)); slotof[i] = (uint8_t)(i & 255u); }
+        ok = ok && hipMemcpy(r->pos.ptr, pos.data(), (size_t)ns * 2, hipMemcpyHostToDevice) == hipSuccess &&
+             hipMemcpy(r->slotof.ptr, slotof.data(), ns, hipMemcpyHostToDevice) == hipSuccess;
     }
     if (!ok) {
         SetError("renderer slot allocation failed (%u slots)", ns);
         r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->smp.release(); r->uv.release(); r->act.release();
-        r->pos.release();
+        r->pos.release(); r->slotof.release(); r->missmask.release();
         delete r;
         return nullptr;
     }
@@ -646,6 +656,8 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     r->slots.smp = r->smp.ptr;
     r->slots.act = r->act.ptr;
     r->slots.pos = r->pos.ptr;
+    r->slots.slotof = r->slotof.ptr;
+    r->slots.missmask = r->missmask.ptr;
     r->slots.spill = nullptr;
     r->slots.n = ns;
     return r;
@@ -661,7 +673,8 @@ void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
     if (!r) return;
     if (d) { (void)hipSetDevice(d->id); (void)hipStreamSynchronize(d->stream); }
     r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->smp.release();
-    r->uv.release(); r->act.release(); r->pos.release(); r->spill.release();
+    r->uv.release(); r->act.release(); r->pos.release(); r->slotof.release(); r->missmask.release();
+    r->spill.release();
     delete r;
 }
 
