@@ -336,12 +336,14 @@ PT_DEV uint32_t SelectBit64(uint64_t m, uint32_t k)
     return pos;
 }
 
-// ShadeOrder: the position shaded by thread u of a tile, hits (and positions
-// outside the image) first in position order, then misses, from the tile's
-// miss mask (extend).  Tile-uniform mask words, no barrier.
-PT_DEV uint32_t ShadePosition(const uint64_t* mask, uint32_t u)
+// ShadeOrder: the position shaded by thread u of a tile: the positions of
+// outcome class 0 first (in position order), then class 1, ... (miss last),
+// from the tile's class masks (extend).  Tile-uniform mask words (scalar
+// loads and counts), no barrier.
+// Two classes (single-material scenes): hits first, then the miss mask.
+PT_DEV uint32_t ShadePosition2(const uint64_t* miss, uint32_t u)
 {
-    uint64_t m0 = mask[0], m1 = mask[1], m2 = mask[2], m3 = mask[3];
+    uint64_t m0 = miss[0], m1 = miss[1], m2 = miss[2], m3 = miss[3];
     uint32_t c0 = (uint32_t)__popcll(~m0), c1 = (uint32_t)__popcll(~m1), c2 = (uint32_t)__popcll(~m2);
     uint32_t nhit = c0 + c1 + c2 + (uint32_t)__popcll(~m3);
     bool hit = u < nhit;
@@ -354,6 +356,34 @@ PT_DEV uint32_t ShadePosition(const uint64_t* mask, uint32_t u)
         if (k >= n1) { k -= n1; word = 2; w = w2;
             if (k >= n2) { k -= n2; word = 3; w = w3; } } }
     return word * 64 + SelectBit64(w, k);
+}
+
+PT_DEV uint32_t ShadePosition(const uint64_t* mask, uint32_t u)
+{
+    uint32_t cnt[PT_OUTCOME_CLASSES][4], before = 0;
+    uint32_t cls = 0, k = u;
+#pragma unroll
+    for (uint32_t c = 0; c < PT_OUTCOME_CLASSES; c++) {
+        uint32_t n = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < 4; w++) {
+            cnt[c][w] = (uint32_t)__popcll(mask[4 * c + w]);
+            n += cnt[c][w];
+        }
+        if (u >= before) { cls = c; k = u - before; }   // last class whose start is <= u
+        before += n;
+    }
+    // Empty classes share their start with the next class, so the last
+    // class starting at or before u holds u.
+    uint32_t word = 0;
+    uint32_t c0 = cnt[0][0], c1 = cnt[0][1], c2 = cnt[0][2];
+#pragma unroll
+    for (uint32_t c = 1; c < PT_OUTCOME_CLASSES; c++)
+        if (cls == c) { c0 = cnt[c][0]; c1 = cnt[c][1]; c2 = cnt[c][2]; }
+    if (k >= c0) { k -= c0; word = 1;
+        if (k >= c1) { k -= c1; word = 2;
+            if (k >= c2) { k -= c2; word = 3; } } }
+    return word * 64 + SelectBit64(mask[4 * cls + word], k);
 }
 
 // TileOrder: called by all 256 threads of a block (one tile) once their new
@@ -603,16 +633,29 @@ struct ray_source_slots {
         L.hit[s] = make_float4(Ln.Time, __uint_as_float(Ln.Shape), __uint_as_float(Ln.Prim), Ln.C.x);
         L.uv[s] = make_float2(Ln.C.y, Ln.C.z);
     }
-    // ShadeOrder: each wave, once all its rays are traced, stores the ballot
-    // of its escaped rays (one word per 64 positions; no atomics, no barrier).
-    PT_DEV void outcome(uint32_t q, uint64_t miss_ballot) const
+    // ShadeOrder: each wave, once all its rays are traced, stores one ballot
+    // per outcome class (one word per 64 positions and class; no atomics,
+    // no barrier).
+    // Single-material scenes store the miss class only (ShadePosition reads
+    // nothing else for them).
+    PT_DEV void outcome(uint32_t q, uint32_t cls, bool classes) const
     {
-        if ((q & 63u) == 0) L.missmask[q >> 6] = miss_ballot;
+        uint64_t* m = L.outcome + (size_t)(q >> 8) * (4 * PT_OUTCOME_CLASSES) + ((q >> 6) & 3u);
+        if (!classes) {
+            uint64_t b = __ballot(cls == PT_OUTCOME_CLASSES - 1);
+            if ((q & 63u) == 0) m[4 * (PT_OUTCOME_CLASSES - 1)] = b;
+            return;
+        }
+#pragma unroll
+        for (uint32_t c = 0; c < PT_OUTCOME_CLASSES; c++) {
+            uint64_t b = __ballot(cls == c);
+            if ((q & 63u) == 0) m[4 * c] = b;
+        }
     }
 };
 
 struct ray_source_arrays {
-    PT_DEV void outcome(uint32_t, uint64_t) const {}
+    PT_DEV void outcome(uint32_t, uint32_t, bool) const {}
     const float* origins;
     const uint32_t* vel;
     const float* dur;
@@ -648,7 +691,7 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
     st.stride = spill_stride;
     pt3 O, V;
     float D;
-    bool miss = false;
+    uint32_t cls = 0;   // ShadeOrder class (positions outside the image: 0, shade skips them)
     if (src.load(slot, O, V, D)) {
         lane_state Ln;
         LaneBegin(S, Ln, O, V, D);
@@ -656,9 +699,16 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
         if (S.g.ShapeCount != 0)
             while (!LaneStep<SPILL, CAP, Src, no_stats, true>(S, Ln, st, src, slot, ns)) {}
         src.store(slot, Ln);
-        miss = Ln.Shape == SHAPE_INDEX_NONE;
+        if (Ln.Shape == SHAPE_INDEX_NONE) {
+            cls = 4;
+        } else if (S.mat_classes) {
+            uint32_t T = S.material[32 * (size_t)S.shapes[Ln.Shape].MaterialIndex];
+            cls = T == PT_MATERIAL_TYPE_BASIC_DIFFUSE ? 0u
+                : T == PT_MATERIAL_TYPE_BASIC_METAL ? 1u
+                : T == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT ? 2u : 3u;
+        }
     }
-    src.outcome(slot, __ballot(miss));
+    src.outcome(slot, cls, S.mat_classes != 0);
 }
 
 PT_DEV uint32_t WaveSum(uint32_t v)
@@ -746,7 +796,9 @@ __global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MIN
     // state is read and written by slot (gathers within the tile's records).
     const uint32_t base = blockIdx.x * 256;
 #if PT_SHADE_ORDER
-    uint32_t s = base | L.slotof[base | ShadePosition(L.missmask + 4 * (size_t)blockIdx.x, threadIdx.x)];
+    const uint64_t* om = L.outcome + (size_t)blockIdx.x * (4 * PT_OUTCOME_CLASSES);
+    uint32_t s = base | L.slotof[base | (S.mat_classes ? ShadePosition(om, threadIdx.x)
+                                                      : ShadePosition2(om + 4 * (PT_OUTCOME_CLASSES - 1), threadIdx.x))];
 #else
     uint32_t s = base | threadIdx.x;
 #endif

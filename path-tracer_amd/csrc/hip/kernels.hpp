@@ -17,6 +17,9 @@ namespace ptd {
 
 struct dscene;
 
+// ShadeOrder outcome classes of a traced ray (kernels.hip).
+constexpr uint32_t PT_OUTCOME_CLASSES = 5;   // hit: diffuse, metal, translucent, other material; miss
+
 // Per-slot state, SoA of 16-byte records.
 struct dslots {
     float4* ray;        // origin.xyz, packed velocity
@@ -29,7 +32,8 @@ struct dslots {
     uint16_t* pos;      // per slot: position of its current ray (high byte) and of
                         // its last traced hit (low byte) within its tile (TileOrder)
     uint8_t* slotof;    // per position: the slot (within the tile) whose ray sits there
-    uint64_t* missmask; // per tile, 4 words: bit t set iff the ray at position t escaped (by extend)
+    uint64_t* outcome;  // ShadeOrder, per tile [class][4 words]: bit t set iff the ray at position t
+                        // ended in that class (extend): hit diffuse / metal / translucent / other, miss
     uint32_t* spill;    // traversal stack spill: (needed - LDS capacity) rows x n
     uint32_t n;
 };

@@ -35,6 +35,7 @@ struct dscene {
     uint32_t atlas_w, atlas_h, atlas_layers;
     uint32_t fast_div;             // every BVH box coordinate is 0 or in [2^-50, 2^40] (IntersectBoundingBox)
     uint32_t blas_words;           // BLAS stack holds packed node words (PackBlasEntry, kernels.hip)
+    uint32_t mat_classes;          // shapes use more than one material type: extend classes hits by type
 };
 
 struct ray { pt3 Origin; pt3 Velocity; float Duration; };

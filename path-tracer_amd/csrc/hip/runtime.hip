@@ -137,7 +137,7 @@ struct pt_basic_renderer {
     dbuf<uint2> act;
     dbuf<uint16_t> pos;                 // TileOrder positions (kernels.hip)
     dbuf<uint8_t> slotof;               // position -> slot within the tile
-    dbuf<uint64_t> missmask;            // ShadeOrder: escaped-ray bits per tile (extend -> shade)
+    dbuf<uint64_t> outcome;             // ShadeOrder: outcome-class bits per tile (extend -> shade)
     dbuf<uint32_t> spill;
 };
 
@@ -514,6 +514,8 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     D.atlas_layers = p->atlas ? p->atlas_layer_count : 0;
     D.fast_div = FastDivBoxes(p) ? 1u : 0u;
     s->mats = SceneMaterialMask(p);
+    uint32_t types = s->mats & (PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_TRANSLUCENT);
+    D.mat_classes = (types & (types - 1)) != 0 ? 1u : 0u;   // more than one material type
     D.blas_words = BlasWordsPackable(p) ? 1u : 0u;
     s->camera_count = p->camera_count;
     s->stack_needed = need;
@@ -627,13 +629,13 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     bool ok = r->ray.alloc(ns) == hipSuccess && r->hit.alloc(ns) == hipSuccess && r->thr.alloc(ns) == hipSuccess &&
               r->prob.alloc(ns) == hipSuccess && r->smp.alloc(ns) == hipSuccess && r->uv.alloc(ns) == hipSuccess &&
               r->act.alloc(ns) == hipSuccess && r->pos.alloc(ns) == hipSuccess && r->slotof.alloc(ns) == hipSuccess &&
-              r->missmask.alloc(ns / 64 + 1) == hipSuccess;
+              r->outcome.alloc((size_t)(ns / 256) * 4 * ptd::PT_OUTCOME_CLASSES + 1) == hipSuccess;
     if (ok && ns) {
         ok = hipMemset(r->ray.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->hit.ptr, 0, (size_t)ns * 16) == hipSuccess &&
              hipMemset(r->thr.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->prob.ptr, 0, (size_t)ns * 16) == hipSuccess &&
              hipMemset(r->smp.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->uv.ptr, 0, (size_t)ns * 8) == hipSuccess &&
              hipMemset(r->act.ptr, 0, (size_t)ns * 8) == hipSuccess &&
-             hipMemset(r->missmask.ptr, 0, (size_t)(ns / 64 + 1) * 8) == hipSuccess;
+             hipMemset(r->outcome.ptr, 0, ((size_t)(ns / 256) * 4 * ptd::PT_OUTCOME_CLASSES + 1) * 8) == hipSuccess;
         // Identity TileOrder until the first Reset sorts the rays.
         std::vector<uint16_t> pos(ns);
         std::vector<uint8_t> slotof(ns);
@@ -644,7 +646,7 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     if (!ok) {
         SetError("renderer slot allocation failed (%u slots)", ns);
         r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->smp.release(); r->uv.release(); r->act.release();
-        r->pos.release(); r->slotof.release(); r->missmask.release();
+        r->pos.release(); r->slotof.release(); r->outcome.release();
         delete r;
         return nullptr;
     }
@@ -657,7 +659,7 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     r->slots.act = r->act.ptr;
     r->slots.pos = r->pos.ptr;
     r->slots.slotof = r->slotof.ptr;
-    r->slots.missmask = r->missmask.ptr;
+    r->slots.outcome = r->outcome.ptr;
     r->slots.spill = nullptr;
     r->slots.n = ns;
     return r;
@@ -673,7 +675,7 @@ void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
     if (!r) return;
     if (d) { (void)hipSetDevice(d->id); (void)hipStreamSynchronize(d->stream); }
     r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->smp.release();
-    r->uv.release(); r->act.release(); r->pos.release(); r->slotof.release(); r->missmask.release();
+    r->uv.release(); r->act.release(); r->pos.release(); r->slotof.release(); r->outcome.release();
     r->spill.release();
     delete r;
 }
