@@ -677,21 +677,21 @@ struct ray_source_arrays {
 
 // Extend: one ray per thread, LaneStep run to completion.  (A persistent
 // variant with per-wave dynamic ray fetch was measured 1.6x slower on C3: the
-// refill bookkeeping cost more than the idle lanes it recovered.)
-template <class Src, bool SPILL, int MINW, int CAP>
-__global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, uint32_t n, uint32_t* spill,
-                                                                  uint32_t spill_stride)
+// refill bookkeeping cost more than the idle lanes it recovered.  Persistent
+// waves claiming 64-ray chunks from a launch-wide counter, each ray traced to
+// completion, were 1.5x slower too (extend 0.592 vs 0.387 ms): a CU's waves
+// then trace unrelated chunks, losing the L1 reuse of a tile's four waves,
+// and the dispatcher already balances the 8100 one-tile blocks.)
+//
+// One ray: Trace() by LaneStep to completion, the compact hit stored, and
+// the ray's ShadeOrder outcome class ballotted (positions outside the image:
+// class 0, shade skips them).
+template <bool SPILL, int CAP, class Src>
+PT_DEV void ExtendRay(const dscene& S, const Src& src, tstack<SPILL, CAP>& st, uint32_t slot)
 {
-    __shared__ uint32_t smem[CAP * 256];
-    uint32_t slot = blockIdx.x * 256 + threadIdx.x;
-    if (slot >= n) return;
-    tstack<SPILL, CAP> st;
-    st.lds = &smem[threadIdx.x];
-    st.spill = spill + slot;
-    st.stride = spill_stride;
     pt3 O, V;
     float D;
-    uint32_t cls = 0;   // ShadeOrder class (positions outside the image: 0, shade skips them)
+    uint32_t cls = 0;
     if (src.load(slot, O, V, D)) {
         lane_state Ln;
         LaneBegin(S, Ln, O, V, D);
@@ -709,6 +709,20 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
         }
     }
     src.outcome(slot, cls, S.mat_classes != 0);
+}
+
+template <class Src, bool SPILL, int MINW, int CAP>
+__global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, uint32_t n, uint32_t* spill,
+                                                                  uint32_t spill_stride)
+{
+    __shared__ uint32_t smem[CAP * 256];
+    uint32_t slot = blockIdx.x * 256 + threadIdx.x;
+    if (slot >= n) return;
+    tstack<SPILL, CAP> st;
+    st.lds = &smem[threadIdx.x];
+    st.spill = spill + slot;
+    st.stride = spill_stride;
+    ExtendRay<SPILL, CAP>(S, src, st, slot);
 }
 
 PT_DEV uint32_t WaveSum(uint32_t v)
