@@ -13,9 +13,13 @@
 //     compressed faces and BVH nodes (:269-316);
 //   * spectrum.dat: {'SPEC', 0} + the compressed RGB->spectrum coefficient
 //     table (:481-509).
-// A compressed block is a native `mz_ulong` (8 bytes on LP64) byte count
-// followed by a zlib stream (mz_compress / mz_uncompress, :16-44): zlib's
-// compress2 / uncompress read and write the same streams.  File names come
+// A compressed block is an `mz_ulong` byte count followed by a zlib stream
+// (mz_compress / mz_uncompress, :16-44): zlib's compress2 / uncompress read
+// and write the same streams.  mz_ulong is `unsigned long`, 4 bytes on the
+// reference's platform: its WriteCompressed calls std::max(Size, 1024ull)
+// (:18), which only compiles where size_t is unsigned long long, i.e. an
+// LLP64 (MSVC x64) build.  So blocks are written with a 4-byte count, and the
+// reader also accepts an 8-byte one.  File names come
 // from MakeFileName (:46-59): every non-alphanumeric character becomes '_'.
 //
 // Deliberate differences, each compatible with the reference's reader:
@@ -362,19 +366,33 @@ bool WriteCompressed(std::ostream& Out, const void* Data, size_t Size)
     uLongf Got = Bound;
     if (compress2(Buf.data(), &Got, static_cast<const Bytef*>(Data), (uLong)Size, Z_DEFAULT_COMPRESSION) != Z_OK)
         return false;
-    uint64_t N = Got;   // mz_ulong (unsigned long, 8 bytes on LP64)
+    if (Got > 0xFFFFFFFFul) return false;   // not representable in the reference's mz_ulong
+    uint32_t N = (uint32_t)Got;
     Out.write(reinterpret_cast<const char*>(&N), sizeof N);
     Out.write(reinterpret_cast<const char*>(Buf.data()), (std::streamsize)Got);
     return (bool)Out;
 }
 
+// Accepts the 4-byte prefix (the reference's platform, and this writer) and
+// an 8-byte one (mz_ulong on an LP64 build of the reference): a zlib stream
+// never starts with a zero byte (CMF's low nibble is 8), while the high half
+// of an 8-byte count below 4 GiB is four zero bytes.
 bool ReadCompressed(std::istream& In, void* Data, size_t Size)
 {
-    uint64_t N = 0;
+    uint32_t N = 0;
+    unsigned char Next[4] = {0, 0, 0, 0};
     In.read(reinterpret_cast<char*>(&N), sizeof N);
-    if (!In || N > (1ull << 40)) return false;
-    std::vector<unsigned char> Buf(std::max<uint64_t>(N, 1));
-    In.read(reinterpret_cast<char*>(Buf.data()), (std::streamsize)N);
+    In.read(reinterpret_cast<char*>(Next), sizeof Next);
+    if (!In) return false;
+    bool Wide = Next[0] == 0 && Next[1] == 0 && Next[2] == 0 && Next[3] == 0;
+    std::vector<unsigned char> Buf(std::max<size_t>(N, 4));
+    size_t Have = 0;
+    if (!Wide) {
+        std::memcpy(Buf.data(), Next, 4);
+        Have = 4;
+    }
+    if (N < Have) return false;
+    In.read(reinterpret_cast<char*>(Buf.data() + Have), (std::streamsize)(N - Have));
     if (!In) return false;
     uLongf Got = (uLongf)Size;
     if (uncompress(static_cast<Bytef*>(Data), &Got, Buf.data(), (uLong)N) != Z_OK) return Size == 0 && N == 0;

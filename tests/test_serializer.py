@@ -3,7 +3,8 @@
 The reference ships no scene files, so the format is pinned by its writer's
 definition: nlohmann dump(4) JSON with sorted keys, object references as
 indices (-1 = null), per-asset binary files with the 'TEX ' / 'MESH' /
-'SPEC' headers and mz_compress (zlib) blocks behind an 8-byte size.  A
+'SPEC' headers and mz_compress (zlib) blocks behind a 4-byte size (mz_ulong
+on the reference's LLP64 platform; an 8-byte size is read as well).  A
 round trip must reproduce every packed buffer the integrator consumes
 byte for byte, and a file written the reference's way (no vertex block, no
 extension keys) must load.
@@ -98,13 +99,15 @@ def test_json_layout(pt, tmp_path):
     raw = (path.parent / "Plane_Texture.texture").read_bytes()
     magic, version, w, h = struct.unpack_from("<4I", raw)
     assert magic == 0x54455820 and raw[:4] == b" XET" and version == 0 and (w, h) == (2, 2)
-    (n,) = struct.unpack_from("<Q", raw, 16)
-    px = np.frombuffer(zlib.decompress(raw[24:24 + n]), np.float32).reshape(4, 4)
+    (n,) = struct.unpack_from("<I", raw, 16)
+    assert len(raw) == 20 + n
+    px = np.frombuffer(zlib.decompress(raw[20:20 + n]), np.float32).reshape(4, 4)
     assert np.array_equal(px, [[1, 1, 1, 1], [.5, .5, .5, 1], [.5, .5, .5, 1], [1, 1, 1, 1]])
     spec = (path.parent / "spectrum.dat").read_bytes()
     assert struct.unpack_from("<2I", spec) == (0x53504543, 0)
-    (n,) = struct.unpack_from("<Q", spec, 8)
-    assert len(zlib.decompress(spec[16:16 + n])) == 3 * 64 * 64 * 64 * 12
+    (n,) = struct.unpack_from("<I", spec, 8)
+    assert len(spec) == 12 + n
+    assert len(zlib.decompress(spec[12:12 + n])) == 3 * 64 * 64 * 64 * 12
     s.close()
 
 
@@ -125,14 +128,16 @@ def test_float_text(pt, tmp_path, value, text):
     s.close()
 
 
-def _compressed(data: bytes) -> bytes:
+def _compressed(data: bytes, width: int = 4) -> bytes:
     z = zlib.compress(data)
-    return struct.pack("<Q", len(z)) + z
+    return struct.pack("<I" if width == 4 else "<Q", len(z)) + z
 
 
-def test_load_reference_written_files(pt, tmp_path):
+@pytest.mark.parametrize("width", [4, 8])
+def test_load_reference_written_files(pt, tmp_path, width):
     """Files as the reference's SaveScene writes them: no extension keys and
-    a .mesh file that ends after the nodes (the reference writes no vertices)."""
+    a .mesh file that ends after the nodes (the reference writes no vertices);
+    block sizes as a 4-byte mz_ulong (its LLP64 build) or an 8-byte one."""
     doc = {
         "Materials": [{"BaseColor": [0.8, 0.3, 0.3], "BaseTexture": -1, "Flags": 0, "Name": "Red",
                        "Opacity": 1.0, "Type": 0}],
@@ -155,8 +160,8 @@ def test_load_reference_written_files(pt, tmp_path):
     faces = np.array([[0, 1, 2]], np.uint32)
     nodes = np.zeros(1, dtype=[("mn", "<f4", 3), ("mx", "<f4", 3), ("fb", "<u4"), ("fe", "<u4"), ("ch", "<u4")])
     nodes[0] = ((0, 0, 0), (1, 1, 0), 0, 1, 0)
-    (tmp_path / "Tri.mesh").write_bytes(struct.pack("<4I", 0x4D455348, 0, 1, 1) + _compressed(faces.tobytes())
-                                        + _compressed(nodes.tobytes()))
+    (tmp_path / "Tri.mesh").write_bytes(struct.pack("<4I", 0x4D455348, 0, 1, 1) + _compressed(faces.tobytes(), width)
+                                        + _compressed(nodes.tobytes(), width))
     s = pt.Scene.load(tmp_path / "ref.json")
     assert s.counts() == (0, 1, 1, 0)
     a = packed(s)
