@@ -13,6 +13,7 @@
 #include <atomic>
 #include <cstring>
 #include <thread>
+#include <cstdlib>
 #include <vector>
 
 namespace {
@@ -1043,8 +1044,14 @@ struct oracle_renderer {
                 for (uint32_t x = 0; x < W; x++) Pixels.push_back(y * W + x);
         State.resize(Pixels.size());
         Accum.assign((size_t)W * H * 4, 0.0f);
+        // threads = 0: OMP_NUM_THREADS when set (the GPU box's CPU share),
+        // else the hardware concurrency, at most 64 either way.
+        if (Threads <= 0) {
+            const char* e = std::getenv("OMP_NUM_THREADS");
+            Threads = e ? std::atoi(e) : 0;
+        }
         if (Threads <= 0) Threads = (int)std::thread::hardware_concurrency();
-        if (Threads <= 0) Threads = 1;
+        Threads = std::max(1, std::min(Threads, 64));
     }
 
     template <class F>

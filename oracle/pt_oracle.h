@@ -23,7 +23,7 @@ extern "C" {
 
 typedef struct oracle_renderer oracle_renderer;
 
-/* Deep-copies the packs. threads = 0: hardware concurrency. */
+/* Deep-copies the packs. threads = 0: OMP_NUM_THREADS, else hardware concurrency (<= 64). */
 oracle_renderer* oracle_create(const pt_scene_packs* packs, uint32_t width, uint32_t height,
                                uint32_t rank, uint32_t nranks, int threads);
 void oracle_destroy(oracle_renderer* r);

@@ -137,6 +137,23 @@ def test_image_rel_l2(pt, dev, config, W, H):
     assert rel <= REL_L2_TOL, f"relative L2 {rel:.3e}"
 
 
+@pytest.mark.parametrize("config,W,H,schedule,camera", [
+    (1, 256, 256, [2] + [1] * 14, 0),    # C1 at its full 256x256, 16 spp
+    (2, 1024, 1024, [2, 1], 0),          # C2 at its full 1024x1024
+    (3, 1920, 1080, [2] + [1] * 6, 0),   # C3 (the bench workload) at its full 1920x1080, 8 rounds
+    (5, 1920, 1080, [2, 1], 0),          # C5 thin-lens camera
+    (5, 1920, 1080, [2, 1], 1),          # C5 360 camera
+])
+def test_full_size_bit_exact(pt, dev, config, W, H, schedule, camera):
+    """BASELINE.json's resolutions: every slot's state and every accumulated
+    pixel bit-exact, over the tile / TileOrder / ShadeOrder layout of a full
+    frame (8100 tiles at 1080p, ragged last tile row)."""
+    gs, os_, ga, oa = render_pair(pt, dev, config, W, H, schedule, camera=camera)
+    compare_state(gs, os_)
+    assert oa[..., 3].sum() > 0
+    assert np.array_equal(ga.view(np.uint32), oa.view(np.uint32))
+
+
 def test_c5_360_camera(pt, dev):
     gs, os_, ga, oa = render_pair(pt, dev, 5, 96, 48, [2, 1, 1], camera=1)
     compare_state(gs, os_)
