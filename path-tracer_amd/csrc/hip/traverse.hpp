@@ -7,6 +7,12 @@
 
 namespace ptd {
 
+// PT_STEP_JOIN: LaneStep's BLAS part as divergent compute + joined state
+// update (below); 0 = the branch-local updates.
+#ifndef PT_STEP_JOIN
+#define PT_STEP_JOIN 1
+#endif
+
 // --- traversal stack: LDS columns + global spill ----------------------------
 
 template <bool SPILL, int CAP>
@@ -125,7 +131,8 @@ PT_DEV void IntersectAnalytic(int32_t Type, pt3 O, pt3 V, uint32_t ShapeIndex, l
 // the edges are the reference's `Position1 - Position0`, `Position2 -
 // Position0`, subtracted once on the host at upload in the same IEEE
 // arithmetic, so every later operation sees identical operands.
-PT_DEV void LaneMeshFace(const dscene& S, uint32_t F, lane_state& L, bool valid = true)
+// The test itself: miss flag, T and the coordinates U, W; L is only read.
+PT_DEV bool FaceTest(const dscene& S, uint32_t F, const lane_state& L, bool valid, float& T, float& U, float& W)
 {
     // valid == false (an empty leaf): face 0 is read and the test forced to
     // miss, instead of a branch around the call.
@@ -149,11 +156,17 @@ PT_DEV void LaneMeshFace(const dscene& S, uint32_t F, lane_state& L, bool valid 
     float InvDet = 1.0f / Det;
 #endif
     pt3 Sv = L.O - P0;
-    float U = InvDet * dot(Sv, RCE2);
+    U = InvDet * dot(Sv, RCE2);
     pt3 SCE1 = cross(Sv, Edge1);
-    float W = InvDet * dot(L.V, SCE1);
-    float T = InvDet * dot(Edge2, SCE1);
-    bool miss = (pt_abs(Det) < PT_EPSILON) | (U < 0) | (U > 1) | (W < 0) | (U + W > 1) | (T < 0) | (T > L.Time) | !valid;
+    W = InvDet * dot(L.V, SCE1);
+    T = InvDet * dot(Edge2, SCE1);
+    return (pt_abs(Det) < PT_EPSILON) | (U < 0) | (U > 1) | (W < 0) | (U + W > 1) | (T < 0) | (T > L.Time) | !valid;
+}
+
+PT_DEV void LaneMeshFace(const dscene& S, uint32_t F, lane_state& L, bool valid = true)
+{
+    float T, U, W;
+    bool miss = FaceTest(S, F, L, valid, T, U, W);
     // Selects, not a branch: the hit registers are updated in place (a
     // conditional update made the compiler keep and copy a second set).
     L.Time = miss ? L.Time : T;
@@ -340,6 +353,67 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
     ss.step();
     const uint32_t* mesh_words = reinterpret_cast<const uint32_t*>(S.mesh_nodes);
     bool tlas = L.blas == SHAPE_INDEX_NONE;
+#if PT_STEP_JOIN
+    if (FACE_STEP && !tlas) {
+        // The divergent part of a BLAS step computes only fresh values (face:
+        // miss flag, T, U, W; internal node: TA, TB and the child words); every
+        // update of the lane state happens after the join, by selects.  State
+        // registers are then written once per step in straight-line code,
+        // instead of being copied around the two exec-masked halves.
+        const bool face = L.nb > 0;
+        bool fmiss = true;
+        float fT = __builtin_nondeterministic_value(0.0f), fU = __builtin_nondeterministic_value(0.0f);
+        float fW = __builtin_nondeterministic_value(0.0f);
+        float TA = __builtin_nondeterministic_value(0.0f), TB = __builtin_nondeterministic_value(0.0f);
+        uint32_t aw0 = __builtin_nondeterministic_value(0u), aw1 = __builtin_nondeterministic_value(0u);
+        uint32_t bw0 = __builtin_nondeterministic_value(0u), bw1 = __builtin_nondeterministic_value(0u);
+        if (face) {
+            fmiss = FaceTest(S, L.na, L, L.na < L.nb, fT, fU, fW);   // (an empty leaf tests nothing)
+            ss.face_step(L.na + 1 >= L.nb);
+        } else {
+            ss.node(true);
+            ss.internal();
+            ss.coherence(L.na);
+            const float4* Np = S.mesh_nodes + 2 * (size_t)L.na;   // child pair: 64 contiguous bytes
+            float4 a0 = Np[0], a1 = Np[1], b0 = Np[2], b1 = Np[3];
+            IntersectBoxPair(L.O, L.V, L.Y, L.Time, a0, a1, b0, b1, L.exact, TA, TB);
+            aw0 = __float_as_uint(a0.w), aw1 = __float_as_uint(a1.w);
+            bw0 = __float_as_uint(b0.w), bw1 = __float_as_uint(b1.w);
+        }
+        L.Time = fmiss ? L.Time : fT;
+        L.Shape = fmiss ? L.Shape : 0xFFFFFFFEu;
+        L.Prim = fmiss ? L.Prim : L.na;
+        L.C = v3(fmiss ? L.C.x : 1 - fU - fW, fmiss ? L.C.y : fU, fmiss ? L.C.z : fW);
+        // Internal node: the reference's three-way decision (scene.glsl.inc:366-392).
+        bool goB = TA > TB;
+        bool push = !face & (goB ? (TA < PT_INFINITY) : (TB < PT_INFINITY));
+        bool moved = face ? (L.na + 1 < L.nb) : (goB | (TA < PT_INFINITY));
+        if (push & (L.dB < 32)) {
+            uint32_t e = S.blas_words ? PackBlasEntry(goB ? aw0 : bw0, goB ? aw1 : bw1) : L.na + (goB ? 0u : 1u);
+            st.put(L.dT + L.dB++, e);
+        }
+        uint32_t na = face ? L.na + 1 : (goB ? bw0 : aw0);
+        uint32_t nb = face ? L.nb : (goB ? bw1 : aw1);
+        if (!moved) {
+            if (L.dB > 0) {
+                ss.pop();
+                uint32_t E = st.get(L.dT + --L.dB);
+                if (S.blas_words) {
+                    UnpackBlasEntry(E, na, nb);
+                } else {
+                    na = mesh_words[8 * E + 3];
+                    nb = mesh_words[8 * E + 7];
+                }
+            } else {
+                tlas = true;
+            }
+        }
+        L.na = na;
+        L.nb = nb;
+        if (!tlas) return false;
+        return TlasStep(S, L, st, src, slot, ss);
+    }
+#endif
     if (!tlas) {
         bool moved = false;
         if (L.nb > 0) {
