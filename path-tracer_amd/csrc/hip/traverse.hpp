@@ -361,12 +361,14 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
         // registers are then written once per step in straight-line code,
         // instead of being copied around the two exec-masked halves.
         const bool face = L.nb > 0;
+        // Each half's outputs start undefined (an empty asm defines them: no
+        // instruction) and are read only by selects that discard them on the
+        // other half's lanes.
         bool fmiss = true;
-        float fT = __builtin_nondeterministic_value(0.0f), fU = __builtin_nondeterministic_value(0.0f);
-        float fW = __builtin_nondeterministic_value(0.0f);
-        float TA = __builtin_nondeterministic_value(0.0f), TB = __builtin_nondeterministic_value(0.0f);
-        uint32_t aw0 = __builtin_nondeterministic_value(0u), aw1 = __builtin_nondeterministic_value(0u);
-        uint32_t bw0 = __builtin_nondeterministic_value(0u), bw1 = __builtin_nondeterministic_value(0u);
+        float fT, fU, fW, TA, TB;
+        uint32_t aw0, aw1, bw0, bw1;
+        asm("" : "=v"(fT), "=v"(fU), "=v"(fW), "=v"(TA), "=v"(TB));
+        asm("" : "=v"(aw0), "=v"(aw1), "=v"(bw0), "=v"(bw1));
         if (face) {
             fmiss = FaceTest(S, L.na, L, L.na < L.nb, fT, fU, fW);   // (an empty leaf tests nothing)
             ss.face_step(L.na + 1 >= L.nb);
