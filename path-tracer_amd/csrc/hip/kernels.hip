@@ -941,14 +941,14 @@ hipError_t pt_launch_raygen(const ptd::dscene& S, const ptd::dslots& L, const pt
 // Occupancy variants of the extend kernel: {min waves per SIMD, LDS stack
 // entries per thread}.  Selected with PT_EXTEND_VARIANT (default 0); stack
 // entries beyond the LDS capacity spill to a global buffer.
-#define PT_EXTEND_VARIANTS(X) X(0, 5, 20) X(1, 4, 24) X(2, 6, 16) X(3, 4, 32)
+#define PT_EXTEND_VARIANTS(X) X(0, 5, 20) X(1, 4, 24) X(2, 6, 16) X(3, 4, 32) X(4, 8, 16) X(5, 8, 12)
 
 int pt_extend_variant()
 {
     static int v = []() {
         const char* e = getenv("PT_EXTEND_VARIANT");
         int x = e ? atoi(e) : 0;
-        return (x >= 0 && x <= 3) ? x : 0;
+        return (x >= 0 && x <= 5) ? x : 0;
     }();
     return v;
 }
@@ -988,14 +988,21 @@ hipError_t pt_launch_extend_stats(const ptd::dscene& S, const ptd::dslots& L, co
 {
     if (L.n == 0) return hipSuccess;
     ptd::ray_source_slots src{L, F};
-    constexpr int CAP = 20;
-    if (pt_extend_stack_cap() != CAP) return hipErrorInvalidConfiguration;
-    if (spill)
-        hipLaunchKernelGGL((ptd::extend_stats_kernel<ptd::ray_source_slots, true, CAP>), dim3(Blocks(L.n)), dim3(256),
-                           0, st, S, src, L.n, spill, L.n, out);
-    else
-        hipLaunchKernelGGL((ptd::extend_stats_kernel<ptd::ray_source_slots, false, CAP>), dim3(Blocks(L.n)),
-                           dim3(256), 0, st, S, src, L.n, spill, L.n, out);
+    // The same LDS stack capacity as the render kernel (the spill buffer is
+    // sized for it).
+    switch (pt_extend_variant()) {
+#define X(id, w, cap)                                                                                           \
+    case id:                                                                                                   \
+        if (spill)                                                                                             \
+            hipLaunchKernelGGL((ptd::extend_stats_kernel<ptd::ray_source_slots, true, cap>), dim3(Blocks(L.n)),  \
+                               dim3(256), 0, st, S, src, L.n, spill, L.n, out);                                \
+        else                                                                                                   \
+            hipLaunchKernelGGL((ptd::extend_stats_kernel<ptd::ray_source_slots, false, cap>), dim3(Blocks(L.n)), \
+                               dim3(256), 0, st, S, src, L.n, spill, L.n, out);                                \
+        break;
+        PT_EXTEND_VARIANTS(X)
+#undef X
+    }
     return hipGetLastError();
 }
 
