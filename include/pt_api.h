@@ -225,6 +225,9 @@ int ptCheckFastReciprocal(pt_device* device, uint64_t* mismatches);
  * taking them: 1, 2, 3-4, 5-8, more than 8}. */
 #define PT_EXTEND_STATS_COUNT 14
 int ptExtendStats(pt_device* device, pt_basic_renderer* renderer, uint64_t out[PT_EXTEND_STATS_COUNT]);
+/* Diagnostic, same pass: the traversal step count of every ray, per ray
+ * POSITION (steps[q], q < width-rounded slot count; 0 where no ray). */
+int ptExtendStepCounts(pt_device* device, pt_basic_renderer* renderer, uint32_t* steps);
 
 /* Per-kernel device time, measured with HIP events on the renderer stream. */
 int ptSetProfiling(pt_device* device, int enable);

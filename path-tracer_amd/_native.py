@@ -239,6 +239,7 @@ HIP_API = {
     "ptCheckFastDivision": (_i32, [_vp, C.c_uint64, _u32, C.POINTER(C.c_uint64)]),
     "ptCheckFastReciprocal": (_i32, [_vp, C.POINTER(C.c_uint64)]),
     "ptExtendStats": (_i32, [_vp, _vp, C.POINTER(C.c_uint64)]),
+    "ptExtendStepCounts": (_i32, [_vp, _vp, _vp]),
     "ptSetProfiling": (_i32, [_vp, _i32]),
     "ptGetKernelStats": (_i32, [_vp, _i32, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
     "ptResetKernelStats": (_i32, [_vp]),

@@ -744,7 +744,8 @@ PT_DEV uint32_t WaveMax(uint32_t v)
 // efficiency of the traversal loop = lane steps / (wave steps x 64).
 template <class Src, bool SPILL, int CAP>
 __global__ __launch_bounds__(256) void extend_stats_kernel(dscene S, Src src, uint32_t n, uint32_t* spill,
-                                                           uint32_t spill_stride, unsigned long long* out)
+                                                           uint32_t spill_stride, unsigned long long* out,
+                                                           uint32_t* steps)
 {
     __shared__ uint32_t smem[CAP * 256];
     uint32_t slot = blockIdx.x * 256 + threadIdx.x;
@@ -764,6 +765,7 @@ __global__ __launch_bounds__(256) void extend_stats_kernel(dscene S, Src src, ui
             while (!LaneStep<SPILL, CAP, Src, lane_stats, true>(S, Ln, st, src, slot, ss)) {}
         src.store(slot, Ln);
     }
+    if (steps && slot < n) steps[slot] = ss.steps;   // per position (0: no ray)
     uint32_t v[14] = {WaveSum(ray), WaveSum(ss.steps), WaveMax(ss.steps) * 64u, WaveSum(ss.internals),
                       WaveSum(ss.leaves), WaveSum(ss.faces), WaveSum(ss.pops), WaveSum(ss.shapes), 1u,
                       WaveSum(ss.uniq[0]), WaveSum(ss.uniq[1]), WaveSum(ss.uniq[2]), WaveSum(ss.uniq[3]),
@@ -984,7 +986,7 @@ static hipError_t LaunchExtend(const ptd::dscene& S, const Src& src, uint32_t n,
 }
 
 hipError_t pt_launch_extend_stats(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* spill,
-                                  unsigned long long* out, hipStream_t st)
+                                  unsigned long long* out, uint32_t* steps, hipStream_t st)
 {
     if (L.n == 0) return hipSuccess;
     ptd::ray_source_slots src{L, F};
@@ -995,10 +997,10 @@ hipError_t pt_launch_extend_stats(const ptd::dscene& S, const ptd::dslots& L, co
     case id:                                                                                                   \
         if (spill)                                                                                             \
             hipLaunchKernelGGL((ptd::extend_stats_kernel<ptd::ray_source_slots, true, cap>), dim3(Blocks(L.n)),  \
-                               dim3(256), 0, st, S, src, L.n, spill, L.n, out);                                \
+                               dim3(256), 0, st, S, src, L.n, spill, L.n, out, steps);                                \
         else                                                                                                   \
             hipLaunchKernelGGL((ptd::extend_stats_kernel<ptd::ray_source_slots, false, cap>), dim3(Blocks(L.n)), \
-                               dim3(256), 0, st, S, src, L.n, spill, L.n, out);                                \
+                               dim3(256), 0, st, S, src, L.n, spill, L.n, out, steps);                                \
         break;
         PT_EXTEND_VARIANTS(X)
 #undef X

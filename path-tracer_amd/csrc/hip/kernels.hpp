@@ -59,7 +59,7 @@ hipError_t pt_launch_raygen(const ptd::dscene& S, const ptd::dslots& L, const pt
 hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* spill,
                             hipStream_t st);
 hipError_t pt_launch_extend_stats(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* spill,
-                                  unsigned long long* out, hipStream_t st);
+                                  unsigned long long* out, uint32_t* steps, hipStream_t st);
 // Material-type mask of a scene (shade kernel specialisation).
 enum : uint32_t {
     PT_MATS_DIFFUSE = 1,

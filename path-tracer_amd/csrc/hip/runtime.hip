@@ -944,23 +944,39 @@ int ptCheckFastReciprocal(pt_device* d, uint64_t* mismatches)
     return 0;
 }
 
-int ptExtendStats(pt_device* d, pt_basic_renderer* r, uint64_t out[PT_EXTEND_STATS_COUNT])
+static int ExtendStats(pt_device* d, pt_basic_renderer* r, uint64_t* out, uint32_t* steps_out, const char* what)
 {
-    if (!d || !out) { SetError("null argument"); return -1; }
+    if (!d || (!out && !steps_out)) { SetError("null argument"); return -1; }
     if (CheckReady(r) != 0) return -1;
     PT_HIP(hipSetDevice(d->id));
     if (int e = EnsureSpill(r)) return e;
     unsigned long long* dm = nullptr;
+    uint32_t* ds = nullptr;
     PT_HIP(hipMalloc(&dm, PT_EXTEND_STATS_COUNT * sizeof(unsigned long long)));
-    hipError_t e = hipMemsetAsync(dm, 0, PT_EXTEND_STATS_COUNT * sizeof(unsigned long long), d->stream);
-    if (e == hipSuccess) e = pt_launch_extend_stats(r->scene->d, r->slots, Frame(r), r->slots.spill, dm, d->stream);
+    hipError_t e = steps_out ? hipMalloc(&ds, (size_t)r->slots.n * 4) : hipSuccess;
+    if (e == hipSuccess) e = hipMemsetAsync(dm, 0, PT_EXTEND_STATS_COUNT * sizeof(unsigned long long), d->stream);
+    if (e == hipSuccess)
+        e = pt_launch_extend_stats(r->scene->d, r->slots, Frame(r), r->slots.spill, dm, ds, d->stream);
     unsigned long long h[PT_EXTEND_STATS_COUNT] = {};
     if (e == hipSuccess) e = hipMemcpyAsync(h, dm, sizeof(h), hipMemcpyDeviceToHost, d->stream);
+    if (e == hipSuccess && ds) e = hipMemcpyAsync(steps_out, ds, (size_t)r->slots.n * 4, hipMemcpyDeviceToHost, d->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
     (void)hipFree(dm);
-    if (e != hipSuccess) { SetError("ptExtendStats: %s", hipGetErrorString(e)); return (int)e; }
-    for (int i = 0; i < PT_EXTEND_STATS_COUNT; i++) out[i] = h[i];
+    if (ds) (void)hipFree(ds);
+    if (e != hipSuccess) { SetError("%s: %s", what, hipGetErrorString(e)); return (int)e; }
+    if (out)
+        for (int i = 0; i < PT_EXTEND_STATS_COUNT; i++) out[i] = h[i];
     return 0;
+}
+
+int ptExtendStats(pt_device* d, pt_basic_renderer* r, uint64_t out[PT_EXTEND_STATS_COUNT])
+{
+    return ExtendStats(d, r, out, nullptr, "ptExtendStats");
+}
+
+int ptExtendStepCounts(pt_device* d, pt_basic_renderer* r, uint32_t* steps)
+{
+    return ExtendStats(d, r, nullptr, steps, "ptExtendStepCounts");
 }
 
 int ptSetProfiling(pt_device* d, int enable)

@@ -229,6 +229,18 @@ class BasicRenderer:
             d[k + "_per_ray"] = d[k] / max(d["rays"], 1)
         return d
 
+    def _slot_count(self) -> int:
+        sb = self.sample_buffer
+        tiles_x, bands = (sb.width + 15) // 16, (sb.height + 15) // 16
+        owned = (bands - self.rank + self.nranks - 1) // self.nranks if bands > self.rank else 0
+        return owned * tiles_x * 256
+
+    def extend_step_counts(self) -> np.ndarray:
+        """Traversal steps of every current ray, per ray position (diagnostic)."""
+        out = np.zeros(self._slot_count(), dtype=np.uint32)
+        _check(N.hip_lib().ptExtendStepCounts(self.device.handle, self._h, out.ctypes.data), "ptExtendStepCounts")
+        return out
+
     def read_state(self) -> np.ndarray:
         sb = self.sample_buffer
         out = np.zeros(sb.width * sb.height, dtype=N.PIXEL_STATE_DTYPE)
