@@ -686,8 +686,8 @@ struct ray_source_arrays {
 // One ray: Trace() by LaneStep to completion, the compact hit stored, and
 // the ray's ShadeOrder outcome class ballotted (positions outside the image:
 // class 0, shade skips them).
-template <bool SPILL, int CAP, class Src>
-PT_DEV void ExtendRay(const dscene& S, const Src& src, tstack<SPILL, CAP>& st, uint32_t slot)
+template <bool SPILL, int CAP, class E, class Src>
+PT_DEV void ExtendRay(const dscene& S, const Src& src, tstack<SPILL, CAP, E>& st, uint32_t slot)
 {
     pt3 O, V;
     float D;
@@ -697,7 +697,7 @@ PT_DEV void ExtendRay(const dscene& S, const Src& src, tstack<SPILL, CAP>& st, u
         LaneBegin(S, Ln, O, V, D);
         no_stats ns;
         if (S.g.ShapeCount != 0)
-            while (!LaneStep<SPILL, CAP, Src, no_stats, true>(S, Ln, st, src, slot, ns)) {}
+            while (!LaneStep<SPILL, CAP, Src, no_stats, true, E>(S, Ln, st, src, slot, ns)) {}
         src.store(slot, Ln);
         if (Ln.Shape == SHAPE_INDEX_NONE) {
             cls = 4;
@@ -711,18 +711,18 @@ PT_DEV void ExtendRay(const dscene& S, const Src& src, tstack<SPILL, CAP>& st, u
     src.outcome(slot, cls, S.mat_classes != 0);
 }
 
-template <class Src, bool SPILL, int MINW, int CAP>
+template <class Src, bool SPILL, int MINW, int CAP, class E = uint32_t>
 __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, uint32_t n, uint32_t* spill,
                                                                   uint32_t spill_stride)
 {
-    __shared__ uint32_t smem[CAP * 256];
+    __shared__ E smem[CAP * 256];
     uint32_t slot = blockIdx.x * 256 + threadIdx.x;
     if (slot >= n) return;
-    tstack<SPILL, CAP> st;
+    tstack<SPILL, CAP, E> st;
     st.lds = &smem[threadIdx.x];
     st.spill = spill + slot;
     st.stride = spill_stride;
-    ExtendRay<SPILL, CAP>(S, src, st, slot);
+    ExtendRay<SPILL, CAP, E>(S, src, st, slot);
 }
 
 PT_DEV uint32_t WaveSum(uint32_t v)
@@ -742,14 +742,14 @@ PT_DEV uint32_t WaveMax(uint32_t v)
 // leaves, faces tested, stack pops, TLAS leaves (shapes), waves, then the
 // internal-BLAS wave steps by distinct node count 1, 2, 3-4, 5-8, >8}.  SIMD
 // efficiency of the traversal loop = lane steps / (wave steps x 64).
-template <class Src, bool SPILL, int CAP>
+template <class Src, bool SPILL, int CAP, class E = uint32_t>
 __global__ __launch_bounds__(256) void extend_stats_kernel(dscene S, Src src, uint32_t n, uint32_t* spill,
                                                            uint32_t spill_stride, unsigned long long* out,
                                                            uint32_t* steps)
 {
-    __shared__ uint32_t smem[CAP * 256];
+    __shared__ E smem[CAP * 256];
     uint32_t slot = blockIdx.x * 256 + threadIdx.x;
-    tstack<SPILL, CAP> st;
+    tstack<SPILL, CAP, E> st;
     st.lds = &smem[threadIdx.x];
     st.spill = spill + slot;
     st.stride = spill_stride;
@@ -762,7 +762,7 @@ __global__ __launch_bounds__(256) void extend_stats_kernel(dscene S, Src src, ui
         lane_state Ln;
         LaneBegin(S, Ln, O, V, D);
         if (S.g.ShapeCount != 0)
-            while (!LaneStep<SPILL, CAP, Src, lane_stats, true>(S, Ln, st, src, slot, ss)) {}
+            while (!LaneStep<SPILL, CAP, Src, lane_stats, true, E>(S, Ln, st, src, slot, ss)) {}
         src.store(slot, Ln);
     }
     if (steps && slot < n) steps[slot] = ss.steps;   // per position (0: no ray)
@@ -943,6 +943,8 @@ hipError_t pt_launch_raygen(const ptd::dscene& S, const ptd::dslots& L, const pt
 // Occupancy variants of the extend kernel: {min waves per SIMD, LDS stack
 // entries per thread}.  Selected with PT_EXTEND_VARIANT (default 0); stack
 // entries beyond the LDS capacity spill to a global buffer.
+// Scenes whose stack entries all fit 16 bits (dscene::stack16) run the same
+// variant with a u16 stack.
 #define PT_EXTEND_VARIANTS(X) X(0, 5, 20) X(1, 4, 24) X(2, 6, 16) X(3, 4, 32) X(4, 8, 16) X(5, 8, 12)
 
 int pt_extend_variant()
@@ -965,19 +967,33 @@ uint32_t pt_extend_stack_cap()
     return 20;
 }
 
+template <class Src, int W, int CAP, class E>
+static void LaunchExtendE(const ptd::dscene& S, const Src& src, uint32_t n, uint32_t* spill, uint32_t pad,
+                          hipStream_t st)
+{
+    if (spill)
+        hipLaunchKernelGGL((ptd::extend_kernel<Src, true, W, CAP, E>), dim3(Blocks(n)), dim3(256), pad, st, S, src, n,
+                           spill, n);
+    else
+        hipLaunchKernelGGL((ptd::extend_kernel<Src, false, W, CAP, E>), dim3(Blocks(n)), dim3(256), pad, st, S, src, n,
+                           spill, n);
+}
+
 template <class Src>
 static hipError_t LaunchExtend(const ptd::dscene& S, const Src& src, uint32_t n, uint32_t* spill, hipStream_t st)
 {
     if (n == 0) return hipSuccess;
+    // PT_EXTEND_LDS_PAD: extra (unused) dynamic LDS per block, an occupancy cap
+    // for experiments (e.g. 12288 -> 5 blocks per CU).
+    static const uint32_t pad = []() {
+        const char* e = getenv("PT_EXTEND_LDS_PAD");
+        return e ? (uint32_t)atoi(e) : 0u;
+    }();
     switch (pt_extend_variant()) {
 #define X(id, w, cap)                                                                                           \
     case id:                                                                                                   \
-        if (spill)                                                                                             \
-            hipLaunchKernelGGL((ptd::extend_kernel<Src, true, w, cap>), dim3(Blocks(n)), dim3(256), 0, st, S,    \
-                               src, n, spill, n);                                                              \
-        else                                                                                                   \
-            hipLaunchKernelGGL((ptd::extend_kernel<Src, false, w, cap>), dim3(Blocks(n)), dim3(256), 0, st, S,   \
-                               src, n, spill, n);                                                              \
+        if (S.stack16) LaunchExtendE<Src, w, cap, uint16_t>(S, src, n, spill, pad, st);                         \
+        else LaunchExtendE<Src, w, cap, uint32_t>(S, src, n, spill, pad, st);                                   \
         break;
         PT_EXTEND_VARIANTS(X)
 #undef X
@@ -985,22 +1001,29 @@ static hipError_t LaunchExtend(const ptd::dscene& S, const Src& src, uint32_t n,
     return hipGetLastError();
 }
 
+template <int CAP, class E>
+static void LaunchExtendStats(const ptd::dscene& S, const ptd::ray_source_slots& src, uint32_t n, uint32_t* spill,
+                              unsigned long long* out, uint32_t* steps, hipStream_t st)
+{
+    if (spill)
+        hipLaunchKernelGGL((ptd::extend_stats_kernel<ptd::ray_source_slots, true, CAP, E>), dim3(Blocks(n)), dim3(256),
+                           0, st, S, src, n, spill, n, out, steps);
+    else
+        hipLaunchKernelGGL((ptd::extend_stats_kernel<ptd::ray_source_slots, false, CAP, E>), dim3(Blocks(n)),
+                           dim3(256), 0, st, S, src, n, spill, n, out, steps);
+}
+
 hipError_t pt_launch_extend_stats(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* spill,
                                   unsigned long long* out, uint32_t* steps, hipStream_t st)
 {
     if (L.n == 0) return hipSuccess;
     ptd::ray_source_slots src{L, F};
-    // The same LDS stack capacity as the render kernel (the spill buffer is
-    // sized for it).
+    // The same LDS stack capacity and entry width as the render kernel.
     switch (pt_extend_variant()) {
 #define X(id, w, cap)                                                                                           \
     case id:                                                                                                   \
-        if (spill)                                                                                             \
-            hipLaunchKernelGGL((ptd::extend_stats_kernel<ptd::ray_source_slots, true, cap>), dim3(Blocks(L.n)),  \
-                               dim3(256), 0, st, S, src, L.n, spill, L.n, out, steps);                                \
-        else                                                                                                   \
-            hipLaunchKernelGGL((ptd::extend_stats_kernel<ptd::ray_source_slots, false, cap>), dim3(Blocks(L.n)), \
-                               dim3(256), 0, st, S, src, L.n, spill, L.n, out, steps);                                \
+        if (S.stack16) LaunchExtendStats<cap, uint16_t>(S, src, L.n, spill, out, steps, st);                    \
+        else LaunchExtendStats<cap, uint32_t>(S, src, L.n, spill, out, steps, st);                              \
         break;
         PT_EXTEND_VARIANTS(X)
 #undef X

@@ -34,7 +34,10 @@ struct dscene {
     const float4* atlas;
     uint32_t atlas_w, atlas_h, atlas_layers;
     uint32_t fast_div;             // every BVH box coordinate is 0 or in [2^-50, 2^40] (IntersectBoundingBox)
-    uint32_t blas_words;           // BLAS stack holds packed node words (PackBlasEntry, kernels.hip)
+    uint32_t blas_words;           // BLAS stack entry format: 0 node index, 1 packed words (PackBlasEntry),
+                                   // 2 16-bit packed words (PackBlasEntry16, blas_firstbits)
+    uint32_t blas_firstbits;       // format 2: bits of a leaf's first face index (count above them)
+    uint32_t stack16;              // every stack entry fits 16 bits: extend runs the u16-stack kernel
     uint32_t mat_classes;          // shapes use more than one material type: extend classes hits by type
 };
 

@@ -448,6 +448,32 @@ static bool BlasWordsPackable(const pt_scene_packs* p)
     return true;
 }
 
+// The 16-bit stack format (PackBlasEntry16): returns the bits F of a leaf's
+// first face index, or 0 if some entry does not fit.  Internal entries are
+// child-pair indices < 2^15; a leaf needs first < 2^F and count < 2^(15-F)
+// for one F; TLAS entries are node indices < 2^16 (ValidatePacks).
+// PT_STACK16=0 disables it.
+static uint32_t BlasWords16FirstBits(const pt_scene_packs* p)
+{
+    const char* e = getenv("PT_STACK16");
+    if (e && atoi(e) == 0) return 0;
+    if (p->shape_node_count > 65536) return 0;
+    uint32_t max_first = 0, max_count = 0;
+    for (uint32_t i = 0; i < p->mesh_node_count; i++) {
+        const pt_packed_mesh_node& n = p->mesh_nodes[i];
+        if (n.FaceEndIndex > 0) {
+            if (n.FaceEndIndex < n.FaceBeginOrNodeIndex) return 0;
+            max_first = std::max(max_first, n.FaceBeginOrNodeIndex);
+            max_count = std::max(max_count, n.FaceEndIndex - n.FaceBeginOrNodeIndex);
+        } else if (n.FaceBeginOrNodeIndex >= 0x8000u) {
+            return 0;
+        }
+    }
+    for (uint32_t F = 1; F < 15; F++)
+        if (max_first < (1u << F) && max_count < (1u << (15 - F))) return F;
+    return 0;
+}
+
 // Material types reachable by a hit (every shape's material) plus whether any
 // medium can scatter: selects the shade kernel instantiation (kernels.hip).
 static uint32_t SceneMaterialMask(const pt_scene_packs* p)
@@ -517,6 +543,13 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     uint32_t types = s->mats & (PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_TRANSLUCENT);
     D.mat_classes = (types & (types - 1)) != 0 ? 1u : 0u;   // more than one material type
     D.blas_words = BlasWordsPackable(p) ? 1u : 0u;
+    D.blas_firstbits = 0;
+    D.stack16 = 0;
+    if (uint32_t F = BlasWords16FirstBits(p)) {   // every stack entry fits 16 bits
+        D.blas_words = 2;
+        D.blas_firstbits = F;
+        D.stack16 = 1;
+    }
     s->camera_count = p->camera_count;
     s->stack_needed = need;
     s->valid = true;

@@ -15,14 +15,14 @@ namespace ptd {
 
 // --- traversal stack: LDS columns + global spill ----------------------------
 
-template <bool SPILL, int CAP>
+template <bool SPILL, int CAP, class E = uint32_t>
 struct tstack {
-    uint32_t* lds;        // &smem[tid]; entry i at lds[i * 256]
+    E* lds;               // &smem[tid]; entry i at lds[i * 256] (E: u32, or u16 when every entry fits)
     uint32_t* spill;      // &spill[thread]; entry i (>= CAP) at spill[(i - CAP) * stride]
     uint32_t stride;
     PT_DEV void put(uint32_t i, uint32_t v)
     {
-        if (!SPILL || i < CAP) lds[i * 256] = v;
+        if (!SPILL || i < CAP) lds[i * 256] = (E)v;
         else spill[(i - CAP) * stride] = v;
     }
     PT_DEV uint32_t get(uint32_t i) const
@@ -240,6 +240,48 @@ PT_DEV void UnpackBlasEntry(uint32_t e, uint32_t& na, uint32_t& nb)
     }
 }
 
+// 16-bit format (dscene::blas_words == 2; the host checks that every entry
+// fits): leaf -> 1<<15 | count<<F | first face, internal -> child-pair index
+// (< 2^15), F = dscene::blas_firstbits.  Half-width LDS stack columns double
+// the blocks a CU can hold (the stack is the extend kernel's LDS).
+PT_DEV uint32_t PackBlasEntry16(uint32_t w0, uint32_t w1, uint32_t F)
+{
+    return w1 > 0 ? (0x8000u | ((w1 - w0) << F) | w0) : w0;
+}
+
+PT_DEV void UnpackBlasEntry16(uint32_t e, uint32_t F, uint32_t& na, uint32_t& nb)
+{
+    uint32_t first = e & ((1u << F) - 1u);
+    bool leaf = (e & 0x8000u) != 0;
+    na = leaf ? first : e;
+    nb = leaf ? first + ((e & 0x7FFFu) >> F) : 0u;
+}
+
+// Push / pop encoding by the scene's format.  The extend kernels run format 2
+// exactly on a u16 stack (dscene::stack16), so there F2 = (SE is u16) is
+// known at compile time; F2_RUNTIME (the preview kernel's u32 stack) checks
+// the format.
+template <class SE, bool F2_RUNTIME = false>
+PT_DEV uint32_t BlasPush(const dscene& S, uint32_t w0, uint32_t w1, uint32_t index)
+{
+    if (sizeof(SE) == 2 || (F2_RUNTIME && S.blas_words == 2)) return PackBlasEntry16(w0, w1, S.blas_firstbits);
+    return S.blas_words ? PackBlasEntry(w0, w1) : index;
+}
+
+template <class SE, bool F2_RUNTIME = false>
+PT_DEV void BlasPop(const dscene& S, uint32_t E, uint32_t& na, uint32_t& nb)
+{
+    if (sizeof(SE) == 2 || (F2_RUNTIME && S.blas_words == 2)) {
+        UnpackBlasEntry16(E, S.blas_firstbits, na, nb);
+    } else if (S.blas_words) {
+        UnpackBlasEntry(E, na, nb);
+    } else {
+        const uint32_t* mesh_words = reinterpret_cast<const uint32_t*>(S.mesh_nodes);
+        na = mesh_words[8 * E + 3];
+        nb = mesh_words[8 * E + 7];
+    }
+}
+
 // Hit.SceneComplexity / Hit.MeshComplexity (scene.glsl.inc:117-118): one count
 // per Intersect / IntersectMeshNode loop iteration = one LaneStep at that level.
 struct complexity_stats {
@@ -266,8 +308,8 @@ struct complexity_stats {
 // The TLAS-level part of a step (scene.glsl.inc:468-520) and the return from
 // a finished BLAS (scene.glsl.inc:409-411); rare on mesh scenes, so LaneStep
 // runs it as one block after the BLAS work instead of as early exits.
-template <bool SPILL, int CAP, class Src, class Stats>
-PT_DEV bool TlasStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, const Src& src, uint32_t slot, Stats& ss)
+template <bool SPILL, int CAP, class Src, class Stats, class SE>
+PT_DEV bool TlasStep(const dscene& S, lane_state& L, tstack<SPILL, CAP, SE>& st, const Src& src, uint32_t slot, Stats& ss)
 {
     const uint32_t* mesh_words = reinterpret_cast<const uint32_t*>(S.mesh_nodes);
     const uint32_t* shape_words = reinterpret_cast<const uint32_t*>(S.shape_nodes);
@@ -346,12 +388,11 @@ PT_DEV bool TlasStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
 // The BLAS work (IntersectMeshNode, scene.glsl.inc:336-399) has no early
 // exit: it ends with the lane either moved to a new node, popped, or handed
 // to TlasStep (BLAS finished, or the lane is at the TLAS level).
-template <bool SPILL, int CAP, class Src, class Stats = no_stats, bool FACE_STEP = false>
-PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, const Src& src, uint32_t slot,
+template <bool SPILL, int CAP, class Src, class Stats = no_stats, bool FACE_STEP = false, class SE = uint32_t>
+PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP, SE>& st, const Src& src, uint32_t slot,
                      Stats& ss)
 {
     ss.step();
-    const uint32_t* mesh_words = reinterpret_cast<const uint32_t*>(S.mesh_nodes);
     bool tlas = L.blas == SHAPE_INDEX_NONE;
 #if PT_STEP_JOIN
     if (FACE_STEP && !tlas) {
@@ -391,21 +432,14 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
         bool push = !face & (goB ? (TA < PT_INFINITY) : (TB < PT_INFINITY));
         bool moved = face ? (L.na + 1 < L.nb) : (goB | (TA < PT_INFINITY));
         if (push & (L.dB < 32)) {
-            uint32_t e = S.blas_words ? PackBlasEntry(goB ? aw0 : bw0, goB ? aw1 : bw1) : L.na + (goB ? 0u : 1u);
-            st.put(L.dT + L.dB++, e);
+            st.put(L.dT + L.dB++, BlasPush<SE>(S, goB ? aw0 : bw0, goB ? aw1 : bw1, L.na + (goB ? 0u : 1u)));
         }
         uint32_t na = face ? L.na + 1 : (goB ? bw0 : aw0);
         uint32_t nb = face ? L.nb : (goB ? bw1 : aw1);
         if (!moved) {
             if (L.dB > 0) {
                 ss.pop();
-                uint32_t E = st.get(L.dT + --L.dB);
-                if (S.blas_words) {
-                    UnpackBlasEntry(E, na, nb);
-                } else {
-                    na = mesh_words[8 * E + 3];
-                    nb = mesh_words[8 * E + 7];
-                }
+                BlasPop<SE>(S, st.get(L.dT + --L.dB), na, nb);
             } else {
                 tlas = true;
             }
@@ -448,8 +482,7 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
             uint32_t aw0 = __float_as_uint(a0.w), aw1 = __float_as_uint(a1.w);
             uint32_t bw0 = __float_as_uint(b0.w), bw1 = __float_as_uint(b1.w);
             if (push & (L.dB < 32)) {
-                uint32_t e = S.blas_words ? PackBlasEntry(goB ? aw0 : bw0, goB ? aw1 : bw1) : Index + (goB ? 0u : 1u);
-                st.put(L.dT + L.dB++, e);
+                st.put(L.dT + L.dB++, BlasPush<SE, !FACE_STEP>(S, goB ? aw0 : bw0, goB ? aw1 : bw1, Index + (goB ? 0u : 1u)));
             }
             if (moved) {
                 L.na = goB ? bw0 : aw0;
@@ -459,13 +492,7 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP>& st, con
         if (!moved) {
             if (L.dB > 0) {
                 ss.pop();
-                uint32_t E = st.get(L.dT + --L.dB);
-                if (S.blas_words) {
-                    UnpackBlasEntry(E, L.na, L.nb);
-                } else {
-                    L.na = mesh_words[8 * E + 3];
-                    L.nb = mesh_words[8 * E + 7];
-                }
+                BlasPop<SE, !FACE_STEP>(S, st.get(L.dT + --L.dB), L.na, L.nb);
             } else {
                 tlas = true;
             }

@@ -87,6 +87,25 @@ def test_trace_rays_bit_exact(pt, dev, config):
     ds.close()
 
 
+@pytest.mark.parametrize("env", [{}, {"PT_STACK16": "0"}, {"PT_STACK16": "0", "PT_BLAS_WORDS": "0"}],
+                         ids=["stack16", "stack32-packed", "stack32-node-index"])
+def test_stack_formats_bit_exact(pt, dev, monkeypatch, env):
+    """Every traversal-stack entry format (chosen per scene at upload: 16-bit
+    packed words, 32-bit packed words, node indices) gives the same hits."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    for config in (3, 5):
+        s = scene_for(pt, config)
+        ds = pt.DeviceScene(dev)
+        ds.update(s)
+        o, v, d = random_rays(s.arrays(), 20000, seed=10 + config)
+        compare_hits(ds.trace_rays(o, v, d), oracle_lib.trace_rays(s.packs(), o, v, d))
+        ds.close()
+    gs, os_, ga, oa = render_pair(pt, dev, 5, 128, 64, [2, 1])
+    compare_state(gs, os_)
+    assert np.array_equal(ga.view(np.uint32), oa.view(np.uint32))
+
+
 def render_pair(pt, dev, config, W, H, schedule, camera=0):
     s = scene_for(pt, config)
     ds = pt.DeviceScene(dev)

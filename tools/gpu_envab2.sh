@@ -6,7 +6,7 @@ CONFIGS=${CONFIGS:-3}
 for set in ${SETTINGS}; do
   vars=""
   [ "$set" = "base" ] || vars=$(echo "$set" | tr ':' ' ')
-  tag=$(echo "$set" | tr ':=' '_-')
+  tag=$(echo "$set" | tr ':=/' '_-_' | tail -c 60)
   timeout -k 10 300 env $vars python -u -m pytest tests/test_gpu_parity.py -q -m gpu -x --timeout 120 --timeout-method thread > gpurun_out/ab_tests_$tag.log 2>&1; rc=$?
   echo "tests [$set] rc=$rc: $(tail -1 gpurun_out/ab_tests_$tag.log)"
   [ $rc -eq 0 ] || exit $rc
