@@ -6,11 +6,12 @@
 // decode RGBE to linear floats with alpha 1.  This decoder follows the PNG
 // (ISO/IEC 15948) and Radiance RGBE specifications and applies those
 // conversions; it reads PNG of every colour type / bit depth (incl. palette,
-// tRNS and Adam7 interlacing) and RLE or flat RGBE .hdr.
+// tRNS and Adam7 interlacing), BMP, TGA and RLE or flat RGBE .hdr.
 #include "image.hpp"
 
 #include <zlib.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -252,6 +253,236 @@ bool DecodeHDR(const std::vector<uint8_t>& f, int& W, int& H, std::vector<vec4>&
     return true;
 }
 
+uint32_t LE16(const uint8_t* p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8; }
+uint32_t LE32(const uint8_t* p) { return LE16(p) | LE16(p + 2) << 16; }
+
+// A 5-bit channel widened to 8 bits the way stb_image's TGA reader does:
+// (v * 255) / 31, integer division.
+uint8_t Widen5(uint32_t v) { return (uint8_t)((v * 255u) / 31u); }
+
+// Truevision TGA (stbi__tga_load semantics): image types 1 / 2 / 3
+// (colour-mapped, true-colour, grey) and their RLE forms 9 / 10 / 11;
+// 8-bit grey or index, 16-bit grey+alpha, 15/16-bit RGB555 (the attribute
+// bit ignored, alpha 255), 24-bit BGR, 32-bit BGRA; palettes of 15/16/24/32-bit
+// entries.  Rows are stored bottom-up unless descriptor bit 5 is set.
+bool DecodeTGA(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_t>& rgba8, std::string& err)
+{
+    if (f.size() < 18) { err = "not a TGA"; return false; }
+    uint32_t idlen = f[0], cmtype = f[1], itype = f[2];
+    uint32_t cmfirst = LE16(&f[3]), cmlen = LE16(&f[5]), cmbits = f[7];
+    uint32_t w = LE16(&f[12]), h = LE16(&f[14]), bits = f[16], desc = f[17];
+    bool rle = itype >= 8;
+    uint32_t base = rle ? itype - 8 : itype;
+    bool mapped = base == 1;
+    if (cmtype > 1 || (base != 1 && base != 2 && base != 3) || (mapped != (cmtype == 1)) || w == 0 || h == 0) {
+        err = "unsupported TGA";
+        return false;
+    }
+    if (mapped ? !(bits == 8 && (cmbits == 15 || cmbits == 16 || cmbits == 24 || cmbits == 32))
+               : base == 3 ? !(bits == 8 || bits == 16)
+                           : !(bits == 15 || bits == 16 || bits == 24 || bits == 32)) {
+        err = "unsupported TGA pixel format";
+        return false;
+    }
+    size_t pos = 18 + idlen;
+    // A pixel (or palette entry) of `b` bits -> RGBA8; grey when `grey`.
+    auto pixel = [](const uint8_t* p, uint32_t b, bool grey, uint8_t* o) {
+        if (grey) {
+            o[0] = o[1] = o[2] = p[0];
+            o[3] = b == 16 ? p[1] : 255;
+        } else if (b == 15 || b == 16) {
+            uint32_t v = LE16(p);
+            o[0] = Widen5((v >> 10) & 31u);
+            o[1] = Widen5((v >> 5) & 31u);
+            o[2] = Widen5(v & 31u);
+            o[3] = 255;
+        } else {
+            o[0] = p[2]; o[1] = p[1]; o[2] = p[0];
+            o[3] = b == 32 ? p[3] : 255;
+        }
+    };
+    std::vector<uint8_t> pal;
+    if (mapped) {
+        // As stb: the colour-map origin is skipped as a byte count and indices
+        // address the stored entries directly (origin 0 in practice), an index
+        // past the map reading entry 0.
+        pos += cmfirst;
+        uint32_t eb = (cmbits + 7) / 8;
+        if (cmlen == 0 || pos + (size_t)cmlen * eb > f.size()) { err = "truncated TGA palette"; return false; }
+        pal.resize((size_t)cmlen * 4);
+        for (uint32_t i = 0; i < cmlen; i++) pixel(&f[pos + (size_t)i * eb], cmbits, false, &pal[4 * (size_t)i]);
+        pos += (size_t)cmlen * eb;
+    } else if (cmtype == 1) {
+        pos += (size_t)cmlen * ((cmbits + 7) / 8);
+    }
+    uint32_t pb = (bits + 7) / 8;
+    size_t n = (size_t)w * h;
+    std::vector<uint8_t> img(n * 4);
+    auto decode = [&](const uint8_t* p, uint8_t* o) -> bool {
+        if (!mapped) { pixel(p, bits, base == 3, o); return true; }
+        uint32_t i = p[0] < cmlen ? p[0] : 0u;
+        std::memcpy(o, &pal[4 * (size_t)i], 4);
+        return true;
+    };
+    for (size_t k = 0; k < n;) {
+        if (!rle) {
+            if (pos + pb > f.size()) { err = "truncated TGA"; return false; }
+            decode(&f[pos], &img[4 * k]);
+            pos += pb;
+            k++;
+            continue;
+        }
+        if (pos >= f.size()) { err = "truncated TGA"; return false; }
+        uint32_t hdr = f[pos++], count = (hdr & 127u) + 1;
+        if (hdr & 128u) {   // run: one pixel repeated
+            if (pos + pb > f.size()) { err = "truncated TGA"; return false; }
+            uint8_t px[4];
+            decode(&f[pos], px);
+            pos += pb;
+            for (uint32_t c = 0; c < count && k < n; c++, k++) std::memcpy(&img[4 * k], px, 4);
+        } else {            // raw packet
+            for (uint32_t c = 0; c < count && k < n; c++, k++) {
+                if (pos + pb > f.size()) { err = "truncated TGA"; return false; }
+                decode(&f[pos], &img[4 * k]);
+                pos += pb;
+            }
+        }
+    }
+    W = (int)w;
+    H = (int)h;
+    rgba8.resize(n * 4);
+    bool top_down = (desc & 0x20u) != 0;
+    for (uint32_t y = 0; y < h; y++) {
+        uint32_t sy = top_down ? y : h - 1 - y;
+        std::memcpy(&rgba8[(size_t)y * w * 4], &img[(size_t)sy * w * 4], (size_t)w * 4);
+    }
+    return true;
+}
+
+// Widens an n-bit field (n <= 8) to 8 bits by bit replication, as stb_image's
+// BMP reader does (stbi__shiftsigned: v * {0xff, 0x55, 0x49, 0x11, 0x21, 0x41,
+// 0x81, 0x01}[n-1] >> {0, 0, 1, 0, 2, 4, 6, 0}[n-1]).
+uint8_t WidenBits(uint32_t v, uint32_t n)
+{
+    static const uint32_t mul[9] = {0, 0xff, 0x55, 0x49, 0x11, 0x21, 0x41, 0x81, 0x01};
+    static const uint32_t sh[9] = {0, 0, 0, 1, 0, 2, 4, 6, 0};
+    return (uint8_t)((v * mul[n]) >> sh[n]);
+}
+
+// Windows BMP (stbi__bmp_load semantics): BITMAPCOREHEADER (12) and
+// BITMAPINFOHEADER and its v2-v5 extensions (40, 52, 56, 108, 124);
+// 1/4/8-bit palettes, 16/32-bit with bit-field masks (defaults 5-5-5 and
+// 8-8-8 when uncompressed), 24-bit BGR; negative height = top-down rows;
+// rows padded to 4 bytes.  A 32-bit image whose alpha is 0 everywhere gets
+// alpha 255 (stb's all-zero-alpha rule).  RLE compression is not supported
+// (stb rejects it too).
+bool DecodeBMP(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_t>& rgba8, std::string& err)
+{
+    if (f.size() < 26 || f[0] != 'B' || f[1] != 'M') { err = "not a BMP"; return false; }
+    uint32_t off = LE32(&f[10]), hsz = LE32(&f[14]);
+    if (hsz != 12 && hsz != 40 && hsz != 52 && hsz != 56 && hsz != 108 && hsz != 124) { err = "unsupported BMP header"; return false; }
+    if (f.size() < 14 + (size_t)hsz) { err = "truncated BMP"; return false; }
+    int32_t w, h;
+    uint32_t bpp, comp = 0;
+    if (hsz == 12) {
+        w = (int16_t)LE16(&f[18]);
+        h = (int16_t)LE16(&f[20]);
+        bpp = LE16(&f[24]);
+    } else {
+        w = (int32_t)LE32(&f[18]);
+        h = (int32_t)LE32(&f[22]);
+        bpp = LE16(&f[28]);
+        comp = LE32(&f[30]);
+    }
+    bool top_down = h < 0;
+    if (top_down) h = -h;
+    if (w <= 0 || h <= 0 || w > (1 << 24) || h > (1 << 24)) { err = "bad BMP size"; return false; }
+    if (comp != 0 && comp != 3) { err = "unsupported BMP compression"; return false; }
+    if (bpp != 1 && bpp != 4 && bpp != 8 && bpp != 16 && bpp != 24 && bpp != 32) { err = "unsupported BMP depth"; return false; }
+    uint32_t mr = 0, mg = 0, mb = 0, ma = 0;
+    size_t pal_pos = 14 + (size_t)hsz;
+    if (bpp == 16 || bpp == 32) {
+        if (comp == 0) {
+            if (bpp == 32) { mr = 0xffu << 16; mg = 0xffu << 8; mb = 0xffu; ma = 0xffu << 24; }
+            else { mr = 31u << 10; mg = 31u << 5; mb = 31u; }
+        } else if (hsz == 40) {   // BI_BITFIELDS: three masks after the header
+            if (f.size() < 14 + 40 + 12) { err = "truncated BMP masks"; return false; }
+            mr = LE32(&f[54]); mg = LE32(&f[58]); mb = LE32(&f[62]);
+            pal_pos += 12;
+        } else if (hsz >= 52) {
+            mr = LE32(&f[54]); mg = LE32(&f[58]); mb = LE32(&f[62]);
+            ma = hsz >= 56 ? LE32(&f[66]) : 0;
+        } else {
+            err = "BMP bit fields without masks";
+            return false;
+        }
+        if (mr == 0 || mg == 0 || mb == 0) { err = "bad BMP masks"; return false; }
+    }
+    std::vector<uint8_t> pal;
+    if (bpp <= 8) {
+        uint32_t es = hsz == 12 ? 3 : 4;
+        size_t entries = off > pal_pos ? (off - pal_pos) / es : 0;
+        entries = std::min<size_t>(entries, 256);
+        if (entries == 0 || pal_pos + entries * es > f.size()) { err = "bad BMP palette"; return false; }
+        pal.resize(entries * 4);
+        for (size_t i = 0; i < entries; i++) {
+            const uint8_t* p = &f[pal_pos + i * es];
+            pal[4 * i] = p[2]; pal[4 * i + 1] = p[1]; pal[4 * i + 2] = p[0]; pal[4 * i + 3] = 255;
+        }
+    }
+    size_t stride = (((size_t)w * bpp + 31) / 32) * 4;
+    if ((size_t)off + stride * (size_t)h > f.size()) { err = "truncated BMP pixels"; return false; }
+    auto field = [](uint32_t v, uint32_t m) -> uint8_t {   // masked field -> 8 bits
+        if (m == 0) return 255;
+        uint32_t s = 0;
+        while (!((m >> s) & 1u)) s++;
+        uint32_t n = 0;
+        while (s + n < 32 && ((m >> (s + n)) & 1u)) n++;
+        uint32_t x = (v & m) >> s;
+        if (n > 8) { x >>= n - 8; n = 8; }
+        return WidenBits(x, n);
+    };
+    W = w;
+    H = h;
+    rgba8.assign((size_t)w * h * 4, 0);
+    bool any_alpha = false;
+    for (int32_t r = 0; r < h; r++) {
+        const uint8_t* row = &f[off + stride * (size_t)r];
+        int32_t y = top_down ? r : h - 1 - r;
+        uint8_t* o = &rgba8[(size_t)y * w * 4];
+        for (int32_t x = 0; x < w; x++, o += 4) {
+            if (bpp <= 8) {
+                uint32_t bit = (uint32_t)x * bpp;
+                uint32_t i = (row[bit / 8] >> (8 - bpp - bit % 8)) & ((1u << bpp) - 1u);
+                if (i < pal.size() / 4) std::memcpy(o, &pal[4 * (size_t)i], 4);
+                else { o[0] = o[1] = o[2] = 0; o[3] = 255; }
+            } else if (bpp == 24) {
+                const uint8_t* p = &row[3 * (size_t)x];
+                o[0] = p[2]; o[1] = p[1]; o[2] = p[0]; o[3] = 255;
+            } else {
+                uint32_t v = bpp == 16 ? LE16(&row[2 * (size_t)x]) : LE32(&row[4 * (size_t)x]);
+                o[0] = field(v, mr); o[1] = field(v, mg); o[2] = field(v, mb);
+                o[3] = field(v, ma);
+                any_alpha |= ma != 0 && o[3] != 0;
+            }
+        }
+    }
+    if (bpp == 32 && ma != 0 && !any_alpha)
+        for (size_t i = 3; i < rgba8.size(); i += 4) rgba8[i] = 255;
+    return true;
+}
+
+// PNG, BMP or TGA (the format without a signature, tried last as stb does).
+bool DecodeLDR(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_t>& rgba8, std::string& err)
+{
+    static const uint8_t png_sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+    if (f.size() >= 8 && std::memcmp(f.data(), png_sig, 8) == 0) return DecodePNG(f, W, H, rgba8, err);
+    if (f.size() >= 2 && f[0] == 'B' && f[1] == 'M') return DecodeBMP(f, W, H, rgba8, err);
+    if (DecodeTGA(f, W, H, rgba8, err)) return true;
+    err = "unsupported image format (PNG, BMP, TGA, Radiance HDR)";
+    return false;
+}
+
 }  // namespace
 
 bool LoadImageFloat(const char* Path, int& Width, int& Height, std::vector<vec4>& Pixels, std::string& Error)
@@ -261,7 +492,7 @@ bool LoadImageFloat(const char* Path, int& Width, int& Height, std::vector<vec4>
     std::vector<uint8_t> f((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
     if (f.size() >= 2 && f[0] == '#' && f[1] == '?') return DecodeHDR(f, Width, Height, Pixels, Error);
     std::vector<uint8_t> rgba8;
-    if (!DecodePNG(f, Width, Height, rgba8, Error)) return false;
+    if (!DecodeLDR(f, Width, Height, rgba8, Error)) return false;
     Pixels.resize((size_t)Width * Height);
     for (size_t i = 0; i < Pixels.size(); i++) {     // stbi__ldr_to_hdr: gamma 2.2 on colour, alpha linear
         const uint8_t* p = &rgba8[4 * i];
@@ -276,7 +507,7 @@ bool LoadImageRGBA8(const char* Path, int& Width, int& Height, std::vector<uint8
     std::ifstream in(Path, std::ios::binary);
     if (!in) { Error = std::string("cannot open ") + Path; return false; }
     std::vector<uint8_t> f((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
-    return DecodePNG(f, Width, Height, RGBA, Error);
+    return DecodeLDR(f, Width, Height, RGBA, Error);
 }
 
 }  // namespace pth
