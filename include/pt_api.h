@@ -158,6 +158,10 @@ int        ptGetDeviceCount(int* count);
 pt_scene* ptCreateScene(pt_device* device);
 int       ptUpdateScene(pt_device* device, pt_scene* scene, const pt_scene_packs* packs, uint32_t dirty_flags);
 void      ptDestroyScene(pt_device* device, pt_scene* scene);
+/* Traversal stack entries the uploaded scene can need (TLAS depth + deepest
+ * BLAS depth, each capped at the reference's Stack[32]); the extend kernel keeps
+ * 20 in LDS and spills the rest to a per-ray global buffer. */
+int       ptSceneStackNeeded(pt_scene* scene, uint32_t* entries);
 
 pt_sample_buffer* ptCreateSampleBuffer(pt_device* device, uint32_t width, uint32_t height);
 void              ptDestroySampleBuffer(pt_device* device, pt_sample_buffer* buffer);

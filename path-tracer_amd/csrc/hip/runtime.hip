@@ -1040,6 +1040,13 @@ int ptResetKernelStats(pt_device* d)
 
 // --- RCCL ------------------------------------------------------------------------
 
+int ptSceneStackNeeded(pt_scene* s, uint32_t* entries)
+{
+    if (!s || !entries) { SetError("null argument"); return -1; }
+    *entries = s->stack_needed;
+    return 0;
+}
+
 int ptCommGetUniqueId(uint8_t id[128])
 {
     static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");

@@ -98,6 +98,13 @@ class DeviceScene:
         packs = scene.packs() if hasattr(scene, "packs") else scene
         _check(N.hip_lib().ptUpdateScene(self.device.handle, self._h, C.byref(packs), dirty_flags), "ptUpdateScene")
 
+    @property
+    def stack_needed(self) -> int:
+        """Traversal stack entries the uploaded scene can need (TLAS + BLAS depth)."""
+        v = C.c_uint32(0)
+        _check(N.hip_lib().ptSceneStackNeeded(self._h, C.byref(v)), "ptSceneStackNeeded")
+        return int(v.value)
+
     def trace_rays(self, origins: np.ndarray, packed_velocities: np.ndarray, durations: np.ndarray) -> np.ndarray:
         """Bit-exact Trace() of a ray batch (scene.glsl.inc:522-611)."""
         o = np.ascontiguousarray(origins, dtype=np.float32).reshape(-1, 3)

@@ -106,6 +106,37 @@ def test_stack_formats_bit_exact(pt, dev, monkeypatch, env):
     assert np.array_equal(ga.view(np.uint32), oa.view(np.uint32))
 
 
+def test_deep_stack_spills_bit_exact(pt, dev, tmp_path):
+    """A scene whose traversal stack outgrows the 20 LDS entries: 24 spheres,
+    each twice the size and distance of the last, build a chain-shaped TLAS
+    (depth 25); rays fired along the chain push every far child, so entries
+    20+ go through the global spill rows.  Hits stay bit-exact."""
+    from test_ingestion import write_model
+    s = pt.Scene.create()
+    for i in range(24):
+        s.create_entity(pt.ENTITY_SPHERE, position=(3.0 * 2.0 ** i, 0.0, 1.0), scale=(0.5 * 2.0 ** i,) * 3)
+    s.instantiate_prefab(s.load_model_as_prefab(write_model(tmp_path)))
+    s.pack()
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    assert ds.stack_needed > 20
+    rng = np.random.default_rng(5)
+    n = 4096
+    o = np.zeros((n, 3), np.float32)
+    o[:, 0] = rng.uniform(-40.0, -2.0, n)
+    o[:, 1:] = rng.normal(0.0, 0.3, (n, 2)) + [0.0, 1.0]
+    d = np.zeros((n, 3))
+    d[:, 0] = 1.0
+    d[:, 1:] = rng.normal(0.0, 0.02, (n, 2))
+    d[n // 2:] = rng.normal(size=(n - n // 2, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    vel = oracle_lib.pack_unit_vectors(d.astype(np.float32))
+    dur = np.full(n, 1048576.0, np.float32)
+    compare_hits(ds.trace_rays(o, vel, dur), oracle_lib.trace_rays(s.packs(), o, vel, dur))
+    ds.close()
+    s.close()
+
+
 def render_pair(pt, dev, config, W, H, schedule, camera=0):
     s = scene_for(pt, config)
     ds = pt.DeviceScene(dev)
