@@ -106,6 +106,8 @@ def main():
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--profile-period", type=int, default=8,
+                    help="time the kernels of every N-th step (HIP events) inside the timed loop")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -154,7 +156,10 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    dev.set_profiling(True)
+    # Kernel durations: HIP events around the extend / shade launches of every
+    # profile_period-th step of the timed loop (an event pair per launch costs
+    # issue time; sampling keeps the measured loop representative).
+    dev.set_profiling(True, period=args.profile_period)
     dev.reset_kernel_stats()
     barrier()
     dev.synchronize()
@@ -259,6 +264,7 @@ def main():
             "alg_bytes_per_launch": ALG_BYTES[dom] * slots_owned,
             "alg_bytes_per_slot": ALG_BYTES[dom],
             "launch_avg_ms": {"extend": round(avg_ext, 4), "shade": round(avg_sh, 4)},
+            "launches_timed": {"extend": n_ext, "shade": n_sh, "every_nth_step": args.profile_period},
             "path_gbps_220B_per_ray": round(PATH_BYTES_PER_RAY * rays / dt / 1e9, 2),
         },
         # What bounds the dominant kernel instead of HBM (PMC, same profile):

@@ -235,6 +235,10 @@ int ptExtendStepCounts(pt_device* device, pt_basic_renderer* renderer, uint32_t*
 
 /* Per-kernel device time, measured with HIP events on the renderer stream. */
 int ptSetProfiling(pt_device* device, int enable);
+/* Time only every period-th ptRunBasicRenderer call (default 1): each event
+ * pair around a kernel costs issue time, so a timed loop can sample its
+ * kernels' durations instead of bracketing every launch. */
+int ptSetProfilingPeriod(pt_device* device, uint32_t period);
 int ptGetKernelStats(pt_device* device, int kernel, uint64_t* launches, double* total_ms);
 int ptResetKernelStats(pt_device* device);
 

@@ -240,6 +240,7 @@ HIP_API = {
     "ptCheckFastReciprocal": (_i32, [_vp, C.POINTER(C.c_uint64)]),
     "ptExtendStats": (_i32, [_vp, _vp, C.POINTER(C.c_uint64)]),
     "ptExtendStepCounts": (_i32, [_vp, _vp, _vp]),
+    "ptSetProfilingPeriod": (_i32, [_vp, C.c_uint32]),
     "ptSceneStackNeeded": (_i32, [_vp, C.POINTER(C.c_uint32)]),
     "ptSetProfiling": (_i32, [_vp, _i32]),
     "ptGetKernelStats": (_i32, [_vp, _i32, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),

@@ -80,6 +80,8 @@ struct pt_device {
     hipStream_t stream = nullptr;
     uint32_t cu_count = 256;
     bool profiling = false;
+    uint32_t profile_period = 1;   // time every period-th Run call
+    uint64_t run_tick = 0;
     std::vector<event_pair> pending;
     std::vector<event_pair> free_events;
     uint64_t launches[PT_KERNEL_COUNT] = {};
@@ -149,9 +151,10 @@ struct pt_comm {
 
 namespace {
 
-int BeginTimed(pt_device* dev, int kernel, event_pair& ep)
+int BeginTimed(pt_device* dev, int kernel, event_pair& ep, bool sampled = true)
 {
-    if (!dev->profiling) return 0;
+    ep.kernel = -1;
+    if (!dev->profiling || !sampled) return 0;
     if (!dev->free_events.empty()) { ep = dev->free_events.back(); dev->free_events.pop_back(); }
     else {
         PT_HIP(hipEventCreate(&ep.a));
@@ -164,7 +167,7 @@ int BeginTimed(pt_device* dev, int kernel, event_pair& ep)
 
 int EndTimed(pt_device* dev, event_pair& ep)
 {
-    if (!dev->profiling) return 0;
+    if (!dev->profiling || ep.kernel < 0) return 0;
     PT_HIP(hipEventRecord(ep.b, dev->stream));
     dev->pending.push_back(ep);
     return 0;
@@ -738,12 +741,13 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
     r->params.FrameIndex += 1;
     ptd::dparams P = Params(r, r->params.FrameIndex);
     ptd::dframe F = Frame(r);
+    bool sampled = d->profiling && (d->run_tick++ % d->profile_period) == 0;
     for (uint32_t i = 0; i < rounds; i++) {
         event_pair ep{};
-        if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep)) return e;
+        if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled)) return e;
         PT_HIP(pt_launch_extend(r->scene->d, r->slots, F, r->slots.spill, d->stream));
         if (int e = EndTimed(d, ep)) return e;
-        if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep)) return e;
+        if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled)) return e;
         PT_HIP(pt_launch_shade(r->scene->d, r->slots, F, P, r->scene->mats, d->stream));
         if (int e = EndTimed(d, ep)) return e;
     }
@@ -1017,6 +1021,14 @@ int ptSetProfiling(pt_device* d, int enable)
     if (!d) { SetError("null device"); return -1; }
     if (int e = CollectTimes(d)) return e;
     d->profiling = enable != 0;
+    return 0;
+}
+
+int ptSetProfilingPeriod(pt_device* d, uint32_t period)
+{
+    if (!d || period == 0) { SetError("bad argument"); return -1; }
+    d->profile_period = period;
+    d->run_tick = 0;
     return 0;
 }
 

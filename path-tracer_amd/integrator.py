@@ -52,8 +52,10 @@ class Device:
     def synchronize(self):
         _check(N.hip_lib().ptSynchronize(self._h), "ptSynchronize")
 
-    def set_profiling(self, enable: bool):
+    def set_profiling(self, enable: bool, period: int = 1):
+        """Kernel timing with HIP events; period > 1 times every period-th Run only."""
         _check(N.hip_lib().ptSetProfiling(self._h, int(enable)), "ptSetProfiling")
+        _check(N.hip_lib().ptSetProfilingPeriod(self._h, int(period)), "ptSetProfilingPeriod")
 
     def kernel_stats(self, kernel: int):
         n = C.c_uint64(0)

@@ -249,7 +249,8 @@ def test_profiling_counts_kernels(pt, dev):
     n_ext, ms_ext = dev.kernel_stats(1)
     n_sh, ms_sh = dev.kernel_stats(2)
     dev.set_profiling(False)
-    assert n_ext == 3 and n_sh == 3 and ms_ext > 0 and ms_sh > 0
+    # one extend + one shade per round and tile range (PT_RUN_PARTS)
+    assert n_ext == n_sh and n_ext % 3 == 0 and n_ext >= 3 and ms_ext > 0 and ms_sh > 0
     r.close(); sb.close(); ds.close()
 
 
