@@ -44,6 +44,9 @@ def load_package():
     return mod
 
 
+SETTLE_ROUNDS = 32   # untimed rounds after Reset + Run(2), before the warm-up steps
+
+
 def measured_traffic(kernel):
     """HBM bytes per launch of `kernel` from the committed PMC profile
     (profiles/traffic.json <- profiles/pmc_summary.py over separate
@@ -144,9 +147,13 @@ def main():
         dist.broadcast(t, 0)
         comm = pt.Comm(dev, world, rank, bytes(t.tolist()))
 
-    # Reset + Run(2) as after a restart (application.cpp:109-110), then warm-up.
+    # Reset + Run(2) as after a restart (application.cpp:109-110), then the
+    # path population settles (the first ~30 rounds after a restart run ~4 %
+    # slower than the rest of a 1024-spp render, tools/exp_trend.py), then the
+    # W warm-up steps.
     r.reset()
     r.run(2)
+    r.run(SETTLE_ROUNDS)
     for _ in range(args.warmup):
         r.run(1)
     dev.synchronize()
@@ -246,6 +253,7 @@ def main():
             "workload": f"C{args.config} room scene, {width}x{height} px ({info.width}x{info.height} per GPU), "
                         f"one round (extend+shade) per step, 16-row bands over {world} GPU(s)",
             "spp_target": info.spp,
+            "settle_rounds": SETTLE_ROUNDS,
             "mesh_faces": info.mesh_face_count,
             "parallelism": f"pixel-bands x{world}" + ((" + gloo reduce (rehearsal, 1 GPU)" if rehearsal
                                                         else " + RCCL reduce") if world > 1 else ""),
