@@ -29,10 +29,17 @@ namespace ptd {
 
 // --- slot / pixel mapping ---------------------------------------------------
 
+// t / tiles_x by the host-computed reciprocal (exact for t * tiles_x < 2^32).
+// (tiles_x == 1: the reciprocal 2^32 does not fit, the row is t itself.)
+PT_DEV uint32_t TileRow(const dframe& F, uint32_t t)
+{
+    return F.tiles_x == 1 ? t : __umulhi(t, F.tiles_x_magic);
+}
+
 PT_DEV bool SlotPixel(const dframe& F, uint32_t s, uint32_t& x, uint32_t& y)
 {
     uint32_t t = s >> 8, l = s & 255u;
-    uint32_t k = t / F.tiles_x;
+    uint32_t k = TileRow(F, t);
     uint32_t tx = t - k * F.tiles_x;
     uint32_t band = F.rank + k * F.nranks;
     x = tx * 16 + (l & 15u);
@@ -45,7 +52,7 @@ PT_DEV bool SlotPixel(const dframe& F, uint32_t s, uint32_t& x, uint32_t& y)
 PT_DEV bool PositionValid(const dframe& F, uint32_t q)
 {
     uint32_t t = q >> 8;
-    uint32_t k = t / F.tiles_x;
+    uint32_t k = TileRow(F, t);
     uint32_t tx = t - k * F.tiles_x;
     uint32_t band = F.rank + k * F.nranks;
     uint32_t nx = min(16u, F.width - tx * 16u);

@@ -43,6 +43,8 @@ struct dframe {
     uint32_t width, height;
     uint32_t rank, nranks;
     uint32_t tiles_x;
+    uint32_t tiles_x_magic;   // ceil(2^32 / tiles_x): t / tiles_x = umulhi(t, magic)
+                              // for t * tiles_x < 2^32 (checked at renderer creation)
 };
 
 struct dparams {

@@ -305,6 +305,7 @@ ptd::dframe Frame(pt_basic_renderer* r)
     F.rank = r->rank;
     F.nranks = r->nranks;
     F.tiles_x = r->tiles_x;
+    F.tiles_x_magic = r->tiles_x > 1 ? (uint32_t)(((1ull << 32) + r->tiles_x - 1) / r->tiles_x) : 0u;
     return F;
 }
 
@@ -660,6 +661,9 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     uint32_t bands = (b->height + 15) / 16;
     uint32_t owned = bands > rank ? (bands - rank + nranks - 1) / nranks : 0;
     uint64_t n = (uint64_t)owned * r->tiles_x * 256;
+    // TileRow's reciprocal division is exact while every tile index t has
+    // t * tiles_x < 2^32.
+    if ((uint64_t)owned * r->tiles_x * r->tiles_x >= (1ull << 32)) { SetError("frame too large"); delete r; return nullptr; }
     if (n > 0xFFFFFFFFull / 2) { SetError("too many slots"); delete r; return nullptr; }
     uint32_t ns = (uint32_t)n;
     bool ok = r->ray.alloc(ns) == hipSuccess && r->hit.alloc(ns) == hipSuccess && r->thr.alloc(ns) == hipSuccess &&

@@ -204,6 +204,15 @@ def test_full_size_bit_exact(pt, dev, config, W, H, schedule, camera):
     assert np.array_equal(ga.view(np.uint32), oa.view(np.uint32))
 
 
+@pytest.mark.parametrize("W,H", [(16, 40), (17, 9), (300, 33)])
+def test_narrow_and_ragged_frames(pt, dev, W, H):
+    """One tile column (the tile-row reciprocal's special case), ragged tile
+    edges in both directions."""
+    gs, os_, ga, oa = render_pair(pt, dev, 1, W, H, [2, 1])
+    compare_state(gs, os_)
+    assert np.array_equal(ga.view(np.uint32), oa.view(np.uint32))
+
+
 def test_c5_360_camera(pt, dev):
     gs, os_, ga, oa = render_pair(pt, dev, 5, 96, 48, [2, 1, 1], camera=1)
     compare_state(gs, os_)
