@@ -25,6 +25,8 @@
 #include "traverse.hpp"
 #include "kernels.hpp"
 
+#include <type_traits>
+
 namespace ptd {
 
 // --- slot / pixel mapping ---------------------------------------------------
@@ -723,13 +725,55 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
                                                                   uint32_t spill_stride)
 {
     __shared__ E smem[CAP * 256];
-    uint32_t slot = blockIdx.x * 256 + threadIdx.x;
+    // Tile order: the slot renderer dispatches the tiles whose waves took
+    // longest in the previous round first (tile_order_kernel), so the
+    // kernel's tail holds short blocks; each wave records its own time.
+    uint32_t tile = blockIdx.x;
+    uint64_t t0 = 0;
+    if constexpr (std::is_same<Src, ray_source_slots>::value) {
+        if (src.L.order) {
+            tile = src.L.order[blockIdx.x];
+            t0 = __builtin_amdgcn_s_memtime();
+        }
+    }
+    uint32_t slot = tile * 256 + threadIdx.x;
     if (slot >= n) return;
     tstack<SPILL, CAP, E> st;
     st.lds = &smem[threadIdx.x];
     st.spill = spill + slot;
     st.stride = spill_stride;
     ExtendRay<SPILL, CAP, E>(S, src, st, slot);
+    if constexpr (std::is_same<Src, ray_source_slots>::value) {
+        if (src.L.order && (threadIdx.x & 63u) == 0)
+            src.L.tilecost[tile * 4 + (threadIdx.x >> 6)] = (uint32_t)(__builtin_amdgcn_s_memtime() - t0);
+    }
+}
+
+// Longest-first dispatch order for the next extend: tiles by their slowest
+// wave's time, descending, by a one-block counting sort over 512 log-spaced
+// buckets (16 per octave).  Any order gives the same results; only the
+// kernel's tail changes.
+__global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, uint32_t* order, uint32_t tiles)
+{
+    __shared__ uint32_t count[512];
+    for (uint32_t i = threadIdx.x; i < 512; i += 1024) count[i] = 0;
+    __syncthreads();
+    auto key = [&](uint32_t t) -> uint32_t {
+        uint32_t c = max(max(cost[4 * t], cost[4 * t + 1]), max(cost[4 * t + 2], cost[4 * t + 3]));
+        if (c < 16) return 511u;                               // untimed / trivial: last
+        uint32_t e = 31u - __clz(c);                           // octave
+        uint32_t m = (c >> (e - 4)) & 15u;                     // 16 steps inside it
+        uint32_t k = min(e * 16u + m, 511u);
+        return 511u - k;                                       // longest first
+    };
+    for (uint32_t t = threadIdx.x; t < tiles; t += 1024) atomicAdd(&count[key(t)], 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t sum = 0;
+        for (uint32_t i = 0; i < 512; i++) { uint32_t c = count[i]; count[i] = sum; sum += c; }
+    }
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < tiles; t += 1024) order[atomicAdd(&count[key(t)], 1u)] = t;
 }
 
 PT_DEV uint32_t WaveSum(uint32_t v)
@@ -1035,6 +1079,13 @@ hipError_t pt_launch_extend_stats(const ptd::dscene& S, const ptd::dslots& L, co
         PT_EXTEND_VARIANTS(X)
 #undef X
     }
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st)
+{
+    if (!L.order || L.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(ptd::tile_order_kernel, dim3(1), dim3(1024), 0, st, L.tilecost, L.order, L.n / 256);
     return hipGetLastError();
 }
 

@@ -34,6 +34,8 @@ struct dslots {
     uint8_t* slotof;    // per position: the slot (within the tile) whose ray sits there
     uint64_t* outcome;  // ShadeOrder, per tile [class][4 words]: bit t set iff the ray at position t
                         // ended in that class (extend): hit diffuse / metal / translucent / other, miss
+    uint32_t* tilecost; // per tile and wave: the wave's extend time (s_memtime ticks)
+    uint32_t* order;    // extend's block -> tile map (longest previous extend first), or null
     uint32_t* spill;    // traversal stack spill: (needed - LDS capacity) rows x n
     uint32_t n;
 };
@@ -78,6 +80,7 @@ hipError_t pt_launch_resolve(const float4* accum, uint32_t n, float brightness, 
                              uint32_t* out8, hipStream_t st);
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
                            uint32_t scene_mats, hipStream_t st);
+hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st);
 hipError_t pt_launch_rcp_check(unsigned long long* mismatches, hipStream_t st);
 hipError_t pt_launch_xdiv_check(uint64_t n, uint32_t seed, unsigned long long* mismatches, hipStream_t st);
 hipError_t pt_launch_trace_rays(const ptd::dscene& S, uint32_t n, const float* origins, const uint32_t* vel,
