@@ -1,4 +1,8 @@
-"""Times C3 rounds without profiling events (PT_RUN_PARTS A/B): Mrays/s."""
+"""Times C3 rounds without profiling events: Mrays/s (best of 3 x 64 rounds).
+
+Used for the multi-stream tile-range experiment recorded in DESIGN.md (the
+PT_RUN_PARTS code was removed after it measured slower) and for checking the
+cost of the kernel-timing events."""
 import sys
 import time
 from pathlib import Path
