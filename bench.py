@@ -1,12 +1,14 @@
 """Benchmark: Mrays/s of the wavefront integrator on the C3 room scene
-(BASELINE.json metric "Mrays/s + Msamples/s, Viking Room 1920x1080 1024spp").
+(BASELINE.json metric "Mrays/s + Msamples/s, Viking Room 1920x1080 1024spp,
+1/2/4/8 GPUs"; --config 4 for C4, 3840x2160 over 8 GPUs).
 
 A step is one integrator round (extend + shade over every pixel slot, i.e.
 one RunBasicRenderer(1)).  Inputs (scene, slot state) are resident in HBM
 before timing starts.  For N GPUs (one process per GPU, launched by
-torch.distributed.run) each rank owns 16-row bands of a 1920 x (1080*N)
-frame, so per-GPU work is fixed (weak scaling); the frame-end RCCL reduce of
-the float4 accumulator to rank 0 is inside the timed region.
+torch.distributed.run) the config's frame is split into 16-row bands, band b
+on rank b % N (strong scaling: the frame is fixed, each rank traces 1/N of
+it); the frame-end exchange (RCCL point-to-point gather of every rank's
+bands to rank 0, ptCommGatherSampleBuffer) is inside the timed region.
 
 Prints ONE JSON line on rank 0.
 """
@@ -69,14 +71,33 @@ def measured_issue(kernel):
     return json.loads(p.read_text()).get("issue", {}).get(kernel)
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(pt, scene, width, height, max_seconds=12.0, max_rounds=200):
     """Time the CPU oracle (scalar C++ restatement, std::thread over host
     cores) on the same scene and frame.  Bounded: Reset + Run(2) warm-up, then
-    single rounds until max_seconds of timed work or max_rounds."""
+    single rounds until max_seconds of timed work or max_rounds.
+
+    Threads: every CPU this process may run on (its affinity mask), capped by
+    OMP_NUM_THREADS when set -- on the GPU box that is the job's CPU share
+    (16) of a machine whose nproc counts every GPU's share."""
     sys.path.insert(0, str(ROOT / "tests"))
     import oracle_lib
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    host_cpus = os.cpu_count() or 1
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = host_cpus
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = max(1, min(allowed, omp) if omp > 0 else allowed)
     o = oracle_lib.OracleRenderer(scene.packs(), width, height, threads=threads)
     o.RenderFlags = 3
     o.reset()
@@ -96,6 +117,11 @@ def cpu_baseline(pt, scene, width, height, max_seconds=12.0, max_rounds=200):
         "value": round((r1 - r0) / dt / 1e6, 4),
         "unit": "Mrays/s",
         "cores": threads,
+        "threads": threads,
+        "host_cpus": host_cpus,
+        "affinity_cpus": allowed,
+        "omp_num_threads": omp or None,
+        "cpu_model": cpu_model(),
         "kind": "port",
         "sample": f"C3 {width}x{height}, {rounds} rounds after Reset+Run(2) warm-up "
                   f"({(r1 - r0)} rays, {(s1 - s0)} samples, {dt:.1f} s)",
@@ -109,16 +135,12 @@ def main():
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--config", type=int, default=3)
-    ap.add_argument("--profile-period", type=int, default=8,
+    ap.add_argument("--profile-period", type=int, default=4,
                     help="time the kernels of every N-th step (HIP events) inside the timed loop")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    # PT_BENCH_REHEARSAL=1: rehearse the multi-rank flow on ONE GPU (every
-    # rank on device 0, frame-end reduce through gloo on host copies, since
-    # RCCL refuses two ranks on one device).  Never used for reported numbers.
-    rehearsal = os.environ.get("PT_BENCH_REHEARSAL") == "1"
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -130,9 +152,9 @@ def main():
     pt = load_package()
     scene = pt.Scene.config(args.config)
     info = scene.info
-    width, height = info.width, info.height * world
+    width, height = info.width, info.height
 
-    dev = pt.Device(0 if rehearsal else local_rank)
+    dev = pt.Device(local_rank)
     dscene = pt.DeviceScene(dev)
     dscene.update(scene)
     sb = pt.SampleBuffer(dev, width, height)
@@ -140,7 +162,7 @@ def main():
     r.RenderFlags = info.render_flags
     r.PathTerminationProbability = info.termination_probability
     comm = None
-    if world > 1 and not rehearsal:
+    if world > 1:
         import torch
         uid = bytearray(pt.Comm.unique_id()) if rank == 0 else bytearray(128)
         t = torch.tensor(list(uid), dtype=torch.uint8)
@@ -157,7 +179,7 @@ def main():
     for _ in range(args.warmup):
         r.run(1)
     dev.synchronize()
-    alpha0 = float(sb.read()[..., 3].sum(dtype=np.float64))
+    rays0, samples0 = r.stats()
 
     def barrier():
         if dist is not None:
@@ -174,13 +196,7 @@ def main():
     for _ in range(args.steps):
         r.run(1)
     if comm is not None:
-        comm.reduce_sample_buffer(sb, 0)
-    elif world > 1:
-        import torch
-        t = torch.from_numpy(sb.read())
-        dist.reduce(t, 0, op=dist.ReduceOp.SUM)
-        if rank == 0:
-            sb.write(t.numpy())
+        comm.gather_sample_buffer(sb, 0)
     dev.synchronize()
     barrier()
     dt = time.perf_counter() - t0
@@ -192,24 +208,21 @@ def main():
     # the timed region; the next Run overwrites the same hit records).
     trav = r.extend_stats()
     slots_owned = int(np.sum(pt.owned_pixels(width, height, rank, world)))
-    acc = sb.read()
-    if world == 1:
-        samples = float(acc[..., 3].sum(dtype=np.float64)) - alpha0
-    else:
-        samples = None   # computed below from the per-rank counts
-
+    # Rays traced and paths completed in the timed steps (ptGetStats; the
+    # sample count equals the accumulator's alpha increments).
+    rays1, samples1 = r.stats()
+    rays_local, samples_local = rays1 - rays0, samples1 - samples0
+    assert rays_local == slots_owned * args.steps
     if dist is not None:
         import torch
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        local = torch.tensor([float(slots_owned), alpha0], dtype=torch.float64)
+        local = torch.tensor([rays_local, samples_local], dtype=torch.float64)
         dist.all_reduce(local, op=dist.ReduceOp.SUM)
-        total_slots, alpha0_total = float(local[0]), float(local[1])
-        if rank == 0:
-            samples = float(acc[..., 3].sum(dtype=np.float64)) - alpha0_total
+        rays, samples = float(local[0]), float(local[1])
     else:
-        total_slots = float(slots_owned)
+        rays, samples = float(rays_local), float(samples_local)
 
     def shutdown():
         for x in (r, sb, dscene):
@@ -224,7 +237,6 @@ def main():
         shutdown()
         return
 
-    rays = total_slots * args.steps
     mrays = rays / dt / 1e6
     avg_ext = ms_ext / max(n_ext, 1)
     avg_sh = ms_sh / max(n_sh, 1)
@@ -235,8 +247,10 @@ def main():
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
     achieved = kernels[dom]["gbps"]
     traffic, traffic_src = measured_traffic(dom)
+    metric = ("Mrays/s + Msamples/s, Viking Room 1920x1080 1024spp, 1/2/4/8 GPUs" if args.config == 3 else
+              f"Mrays/s + Msamples/s, C{args.config} {info.width}x{info.height} {info.spp}spp")
     out = {
-        "metric": "Mrays/s (Viking Room 1920x1080, 1024spp)",
+        "metric": metric,
         "value": round(mrays, 3),
         "unit": "Mrays/s",
         "n_gpus": world,
@@ -244,21 +258,20 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": f"synthetic (procedural {info.mesh_face_count}-triangle room mesh + 1024^2 texture; "
                 "Viking Room asset absent)",
         "config": {
-            "workload": f"C{args.config} room scene, {width}x{height} px ({info.width}x{info.height} per GPU), "
-                        f"one round (extend+shade) per step, 16-row bands over {world} GPU(s)",
+            "workload": f"C{args.config} scene, {width}x{height} px frame split in 16-row bands over {world} GPU(s) "
+                        f"({slots_owned} px on rank 0), one round (extend+shade of every pixel's path) per step",
             "spp_target": info.spp,
             "settle_rounds": SETTLE_ROUNDS,
             "mesh_faces": info.mesh_face_count,
-            "parallelism": f"pixel-bands x{world}" + ((" + gloo reduce (rehearsal, 1 GPU)" if rehearsal
-                                                        else " + RCCL reduce") if world > 1 else ""),
+            "parallelism": f"pixel-bands x{world}" + (" + RCCL band gather to rank 0" if world > 1 else ""),
         },
-        "msamples_per_s": round(samples / dt / 1e6, 3) if samples is not None else None,
+        "msamples_per_s": round(samples / dt / 1e6, 3),
         "roofline": {
             "bound": "hbm",
             "kernel": dom,
@@ -279,6 +292,7 @@ def main():
         # fraction of the chip's VALU issue slots used, and active lanes per
         # VALU instruction (of 64; divergence).
         "limiter": {"kind": "valu_issue", "kernel": dom, **(measured_issue(dom) or {}),
+                    "per_kernel": {k: measured_issue(k) for k in ("extend", "shade")},
                     "source": traffic_src},
     }
     # Node/face bytes the traversal pulls through L1/L2 per ray (BVH + faces

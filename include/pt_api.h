@@ -188,6 +188,10 @@ pt_basic_renderer_params* ptBasicRendererParams(pt_basic_renderer* renderer);
 int                ptResetBasicRenderer(pt_device* device, pt_basic_renderer* renderer);
 int                ptRunBasicRenderer(pt_device* device, pt_basic_renderer* renderer, uint32_t rounds);
 uint32_t           ptBasicRendererSlotCount(pt_basic_renderer* renderer);
+/* Work done since the last Reset: rays traced (one per owned pixel per round)
+ * and paths completed (accumulator sample increments, basic_scatter.glsl:
+ * 350-359).  Either pointer may be NULL.  Synchronises the device stream. */
+int                ptGetStats(pt_device* device, pt_basic_renderer* renderer, uint64_t* rays, uint64_t* samples);
 /* out = width*height states in image order; pixels outside the renderer's
  * partition are left untouched. */
 int                ptReadBasicRendererState(pt_device* device, pt_basic_renderer* renderer, pt_pixel_state* out);
@@ -247,8 +251,18 @@ int      ptCommGetUniqueId(uint8_t id[128]);
 pt_comm* ptCommCreate(pt_device* device, int nranks, int rank, const uint8_t id[128]);
 void     ptCommDestroy(pt_comm* comm);
 /* Frame-end ncclReduce(sum) of the float4 accumulator to `root` (exact: the
- * ranks' pixel bands are disjoint). */
+ * ranks' pixel bands are disjoint).  Each rank first zeroes the rows outside
+ * the bands of the last partitioned renderer created on the buffer, so the
+ * root's buffer may be reduced again after further rounds (progressive
+ * frames): after every call it holds the sum of the ranks' own bands. */
 int      ptCommReduceSampleBuffer(pt_device* device, pt_comm* comm, pt_sample_buffer* buffer, int root);
+/* The same frame-end exchange at 1/N of the traffic: every rank's own bands
+ * go point-to-point to `root`, which stores them in place (grouped
+ * ncclSend/ncclRecv).  Requires the buffer's partition (the last partitioned
+ * renderer created on it) to be this communicator's rank of nranks.  After
+ * the call the root's buffer holds every rank's bands; other ranks' buffers
+ * are unchanged.  Repeatable after further rounds. */
+int      ptCommGatherSampleBuffer(pt_device* device, pt_comm* comm, pt_sample_buffer* buffer, int root);
 
 #ifdef __cplusplus
 }

@@ -93,6 +93,12 @@ void        ptsSetCameraPinhole(pts_scene* scene, pts_entity* camera, float fov_
 void        ptsSetCameraThinLens(pts_scene* scene, pts_entity* camera, float sensor_w_mm, float sensor_h_mm,
                                  float focal_length_mm, float aperture_mm, float focus_distance);
 void        ptsSetCamera360(pts_scene* scene, pts_entity* camera);
+/* The camera entity packed at `packed_index` by the last PackSceneData (NULL
+ * if none), and a camera move as the editor's fly controls make it
+ * (application.cpp:52-66): position / rotation (may be NULL) and only
+ * SCENE_DIRTY_CAMERAS set. */
+pts_entity* ptsFindCamera(pts_scene* scene, uint32_t packed_index);
+void        ptsSetCameraTransform(pts_scene* scene, pts_entity* camera, const float position[3], const float rotation[3]);
 /* root_entity fields (scene.hpp:254-262). */
 void        ptsSetRootParameters(pts_scene* scene, float scatter_rate, float skybox_brightness,
                                  float skybox_sampling_probability, pts_texture* skybox);

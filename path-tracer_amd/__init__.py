@@ -9,7 +9,9 @@ from .scene import (Scene, spectrum_coefficients, build_spectrum_table, load_spe
                     mesh_node_count, ENTITY_CONTAINER, ENTITY_CAMERA, ENTITY_MESH_INSTANCE, ENTITY_PLANE,
                     ENTITY_SPHERE, ENTITY_CUBE, MATERIAL_BASIC_DIFFUSE, MATERIAL_BASIC_METAL,
                     MATERIAL_BASIC_TRANSLUCENT, MATERIAL_OPENPBR, TEXTURE_RAW, TEXTURE_REFLECTANCE_WITH_ALPHA,
-                    TEXTURE_RADIANCE, SCENE_DIRTY_ALL, RENDER_FLAG_ACCUMULATE, RENDER_FLAG_SAMPLE_JITTER)
+                    TEXTURE_RADIANCE, SCENE_DIRTY_ALL, SCENE_DIRTY_GLOBALS, SCENE_DIRTY_TEXTURES,
+                    SCENE_DIRTY_MATERIALS, SCENE_DIRTY_SHAPES, SCENE_DIRTY_MESHES, SCENE_DIRTY_CAMERAS,
+                    SCENE_DIRTY_SKYBOX_TEXTURE, RENDER_FLAG_ACCUMULATE, RENDER_FLAG_SAMPLE_JITTER)
 from .integrator import (Device, DeviceScene, SampleBuffer, BasicRenderer, Comm, PathTracerError, ResolveParameters,
                          device_count, CreateSampleBuffer, CreateBasicRenderer, ResetBasicRenderer, RunBasicRenderer,
                          DestroyBasicRenderer, DestroySampleBuffer, RenderSampleBuffer, PreviewParameters,

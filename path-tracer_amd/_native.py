@@ -168,6 +168,8 @@ SCENE_API = {
     "ptsSetCameraPinhole": (None, [_vp, _vp, _f32, _f32]),
     "ptsSetCameraThinLens": (None, [_vp, _vp, _f32, _f32, _f32, _f32, _f32]),
     "ptsSetCamera360": (None, [_vp, _vp]),
+    "ptsFindCamera": (_vp, [_vp, _u32]),
+    "ptsSetCameraTransform": (None, [_vp, _vp, _fptr, _fptr]),
     "ptsSetRootParameters": (None, [_vp, _f32, _f32, _f32, _vp]),
     "ptsCreateMaterial": (_vp, [_vp, _i32, C.c_char_p]),
     "ptsSetMaterialParameter": (_i32, [_vp, _vp, C.c_char_p, _fptr, _i32]),
@@ -228,6 +230,7 @@ HIP_API = {
     "ptResetBasicRenderer": (_i32, [_vp, _vp]),
     "ptRunBasicRenderer": (_i32, [_vp, _vp, _u32]),
     "ptBasicRendererSlotCount": (_u32, [_vp]),
+    "ptGetStats": (_i32, [_vp, _vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "ptReadBasicRendererState": (_i32, [_vp, _vp, _vp]),
     "ptTraceRays": (_i32, [_vp, _vp, _u32, _fptr, _u32ptr, _fptr, _vp]),
     "ptCreatePreviewRenderContext": (_vp, [_vp, _vp]),
@@ -249,6 +252,7 @@ HIP_API = {
     "ptCommCreate": (_vp, [_vp, _i32, _i32, C.POINTER(C.c_uint8)]),
     "ptCommDestroy": (None, [_vp]),
     "ptCommReduceSampleBuffer": (_i32, [_vp, _vp, _vp, _i32]),
+    "ptCommGatherSampleBuffer": (_i32, [_vp, _vp, _vp, _i32]),
 }
 
 _scene_lib = None

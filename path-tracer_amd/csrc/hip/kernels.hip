@@ -776,6 +776,16 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, 
     for (uint32_t t = threadIdx.x; t < tiles; t += 1024) order[atomicAdd(&count[key(t)], 1u)] = t;
 }
 
+__global__ __launch_bounds__(256) void zero_unowned_kernel(float4* accum, uint32_t width, uint32_t height,
+                                                           uint32_t rank, uint32_t nranks)
+{
+    for (uint32_t y = blockIdx.y; y < height; y += gridDim.y) {
+        if (((y >> 4) % nranks) == rank) continue;
+        for (uint32_t x = blockIdx.x * 256 + threadIdx.x; x < width; x += gridDim.x * 256)
+            accum[(size_t)y * width + x] = make_float4(0, 0, 0, 0);
+    }
+}
+
 PT_DEV uint32_t WaveSum(uint32_t v)
 {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -876,6 +886,7 @@ __global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MIN
     bool valid = SlotPixel(F, s, x, y);
     uint32_t p16 = L.pos[s];
     pt3 O = v3s(0), V = v3s(0);
+    bool completed = false;
     if (valid) {
         rng G;
         G.State = pt_seed(x, y, Pm.seed);
@@ -934,9 +945,14 @@ __global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MIN
                 Val.x = Val.x + Old.x; Val.y = Val.y + Old.y; Val.z = Val.z + Old.z; Val.w = Val.w + Old.w;
             }
             *A = Val;
+            completed = true;
             GenerateNewPath(S, L, F, Pm, G, s, x, y, O, V);
         }
     }
+    // Completed paths per wave (ptGetStats): one counter word per 64 slots,
+    // updated by the wave's first lane (no atomics: a wave owns its word).
+    uint64_t cm = __ballot(completed);
+    if ((threadIdx.x & 63u) == 0) L.done[(base | threadIdx.x) >> 6] += (uint32_t)__popcll(cm);
     TileOrderStoreRay(L, s, valid, O, V, p16 >> 8);
 }
 
@@ -1089,6 +1105,15 @@ hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st)
 {
     if (!L.order || L.n == 0) return hipSuccess;
     hipLaunchKernelGGL(ptd::tile_order_kernel, dim3(1), dim3(1024), 0, st, L.tilecost, L.order, L.n / 256);
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_zero_unowned(float4* accum, uint32_t width, uint32_t height, uint32_t rank, uint32_t nranks,
+                                  hipStream_t st)
+{
+    if (nranks <= 1 || width == 0 || height == 0) return hipSuccess;
+    hipLaunchKernelGGL(ptd::zero_unowned_kernel, dim3(Blocks(width), height < 32768u ? height : 32768u), dim3(256), 0, st, accum, width, height,
+                       rank, nranks);
     return hipGetLastError();
 }
 

@@ -36,6 +36,7 @@ struct dslots {
                         // ended in that class (extend): hit diffuse / metal / translucent / other, miss
     uint32_t* tilecost; // per tile and wave: the wave's extend time (s_memtime ticks)
     uint32_t* order;    // extend's block -> tile map (longest previous extend first), or null
+    uint32_t* done;     // per wave of 64 slots: paths completed by shade since the last Reset (ptGetStats)
     uint32_t* spill;    // traversal stack spill: (needed - LDS capacity) rows x n
     uint32_t n;
 };
@@ -81,6 +82,10 @@ hipError_t pt_launch_resolve(const float4* accum, uint32_t n, float brightness, 
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
                            uint32_t scene_mats, hipStream_t st);
 hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st);
+// Zeroes the rows of a sample buffer outside a renderer's 16-row bands
+// (b % nranks != rank) before a frame-end reduce.
+hipError_t pt_launch_zero_unowned(float4* accum, uint32_t width, uint32_t height, uint32_t rank, uint32_t nranks,
+                                  hipStream_t st);
 hipError_t pt_launch_rcp_check(unsigned long long* mismatches, hipStream_t st);
 hipError_t pt_launch_xdiv_check(uint64_t n, uint32_t seed, unsigned long long* mismatches, hipStream_t st);
 hipError_t pt_launch_trace_rays(const ptd::dscene& S, uint32_t n, const float* origins, const uint32_t* vel,

@@ -113,6 +113,7 @@ struct pt_sample_buffer {
     dbuf<float4> display;      // resolved image (ptRenderSampleBuffer)
     dbuf<uint32_t> display8;   // its sRGB8 encoding
     bool resolved = false;
+    uint32_t rank = 0, nranks = 1;   // pixel bands of the last partitioned renderer created on it
 };
 
 struct pt_preview {
@@ -142,6 +143,9 @@ struct pt_basic_renderer {
     dbuf<uint64_t> outcome;             // ShadeOrder: outcome-class bits per tile (extend -> shade)
     dbuf<uint32_t> tilecost, order;     // longest-first tile order (extend -> tile_order -> extend)
     uint64_t order_tick = 0;            // rounds since creation (tile-order re-sort period)
+    dbuf<uint32_t> done;                // per wave: completed paths since the last Reset (ptGetStats)
+    uint64_t pixels = 0;                // image pixels owned (valid slots)
+    uint64_t rays = 0;                  // rays traced since the last Reset
     dbuf<uint32_t> spill;
 };
 
@@ -691,12 +695,13 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
               r->prob.alloc(ns) == hipSuccess && r->smp.alloc(ns) == hipSuccess && r->uv.alloc(ns) == hipSuccess &&
               r->act.alloc(ns) == hipSuccess && r->pos.alloc(ns) == hipSuccess && r->slotof.alloc(ns) == hipSuccess &&
               r->outcome.alloc((size_t)(ns / 256) * 4 * ptd::PT_OUTCOME_CLASSES + 1) == hipSuccess &&
-              r->tilecost.alloc((size_t)(ns / 256) * 4 + 1) == hipSuccess && r->order.alloc(ns / 256 + 1) == hipSuccess;
+              r->tilecost.alloc((size_t)(ns / 256) * 4 + 1) == hipSuccess && r->order.alloc(ns / 256 + 1) == hipSuccess &&
+              r->done.alloc(ns / 64 + 1) == hipSuccess;
     if (ok && ns) {
         ok = hipMemset(r->ray.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->hit.ptr, 0, (size_t)ns * 16) == hipSuccess &&
              hipMemset(r->thr.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->prob.ptr, 0, (size_t)ns * 16) == hipSuccess &&
              hipMemset(r->smp.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->uv.ptr, 0, (size_t)ns * 8) == hipSuccess &&
-             hipMemset(r->act.ptr, 0, (size_t)ns * 8) == hipSuccess &&
+             hipMemset(r->act.ptr, 0, (size_t)ns * 8) == hipSuccess && hipMemset(r->done.ptr, 0, (size_t)(ns / 64 + 1) * 4) == hipSuccess &&
              hipMemset(r->outcome.ptr, 0, ((size_t)(ns / 256) * 4 * ptd::PT_OUTCOME_CLASSES + 1) * 8) == hipSuccess;
         // Identity TileOrder until the first Reset sorts the rays.
         std::vector<uint16_t> pos(ns);
@@ -713,6 +718,7 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
         SetError("renderer slot allocation failed (%u slots)", ns);
         r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->smp.release(); r->uv.release(); r->act.release();
         r->pos.release(); r->slotof.release(); r->outcome.release(); r->tilecost.release(); r->order.release();
+        r->done.release();
         delete r;
         return nullptr;
     }
@@ -728,8 +734,13 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     r->slots.outcome = r->outcome.ptr;
     r->slots.tilecost = r->tilecost.ptr;
     r->slots.order = TileOrderEnabled() && ns ? r->order.ptr : nullptr;
+    r->slots.done = r->done.ptr;
     r->slots.spill = nullptr;
     r->slots.n = ns;
+    for (uint32_t band = rank; band < bands; band += nranks)
+        r->pixels += (uint64_t)b->width * std::min<uint32_t>(16u, b->height - band * 16u);
+    b->rank = rank;
+    b->nranks = nranks;
     return r;
 }
 
@@ -745,6 +756,7 @@ void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
     r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->smp.release();
     r->uv.release(); r->act.release(); r->pos.release(); r->slotof.release(); r->outcome.release();
     r->tilecost.release(); r->order.release();
+    r->done.release();
     r->spill.release();
     delete r;
 }
@@ -761,7 +773,10 @@ int ptResetBasicRenderer(pt_device* d, pt_basic_renderer* r)
     event_pair ep{};
     if (int e = BeginTimed(d, PT_KERNEL_RAYGEN, ep)) return e;
     PT_HIP(pt_launch_raygen(r->scene->d, r->slots, Frame(r), Params(r, r->params.FrameIndex), d->stream));
-    return EndTimed(d, ep);
+    if (int e = EndTimed(d, ep)) return e;
+    PT_HIP(hipMemsetAsync(r->done.ptr, 0, (size_t)(r->slots.n / 64 + 1) * 4, d->stream));
+    r->rays = 0;
+    return 0;
 }
 
 // RunBasicRenderer (basic.cpp:306-332)
@@ -786,6 +801,27 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
         // Tiles keep their relative cost for many rounds: re-sort every
         // TileOrderPeriod() rounds (the sort is one small launch).
         if (r->slots.order && (r->order_tick++ % TileOrderPeriod()) == 0) PT_HIP(pt_launch_tile_order(r->slots, d->stream));
+        r->rays += r->pixels;
+    }
+    return 0;
+}
+
+// Counters of the work done since the last Reset: rays traced (every owned
+// pixel's slot traces one ray per round, K3) and paths completed (the
+// accumulator increments of basic_scatter.glsl:350-359, counted whether or
+// not RENDER_FLAG_ACCUMULATE is set).  Synchronises the device stream.
+int ptGetStats(pt_device* d, pt_basic_renderer* r, uint64_t* rays, uint64_t* samples)
+{
+    if (!d || !r) { SetError("null argument"); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    PT_HIP(hipStreamSynchronize(d->stream));
+    if (rays) *rays = r->rays;
+    if (samples) {
+        std::vector<uint32_t> w(r->slots.n / 64 + 1);
+        PT_HIP(hipMemcpy(w.data(), r->done.ptr, w.size() * 4, hipMemcpyDeviceToHost));
+        uint64_t sum = 0;
+        for (uint32_t v : w) sum += v;
+        *samples = sum;
     }
     return 0;
 }
@@ -1132,8 +1168,48 @@ int ptCommReduceSampleBuffer(pt_device* d, pt_comm* c, pt_sample_buffer* b, int 
     if (!d || !c || !b) { SetError("null argument"); return -1; }
     PT_HIP(hipSetDevice(d->id));
     size_t count = (size_t)b->width * b->height * 4;
+    // Only the bands this rank renders may enter the sum: at the root the
+    // other rows hold the previous reduce's totals (a progressive frame
+    // reduces again after more rounds), so they are zeroed first and the
+    // in-place sum stays exact on every call.
+    PT_HIP(pt_launch_zero_unowned(b->accum, b->width, b->height, b->rank, b->nranks, d->stream));
     ncclResult_t e = ncclReduce(b->accum, b->accum, count, ncclFloat32, ncclSum, root, c->comm, d->stream);
     if (e != ncclSuccess) { SetError("ncclReduce: %s", ncclGetErrorString(e)); return (int)e; }
+    return 0;
+}
+
+// The same frame-end exchange with 1/N of the traffic: the bands are
+// disjoint, so the root needs only each band's owner's rows.  Band b (rows
+// [16b, 16b+16), contiguous in the row-major buffer) is owned by rank
+// b % nranks; every non-root owner sends its bands to the root, which
+// receives them in place.  One group of point-to-point transfers: each peer
+// pushes ~1/N of the frame over its own xGMI link to the root concurrently,
+// instead of a ring reduction of the whole buffer.
+int ptCommGatherSampleBuffer(pt_device* d, pt_comm* c, pt_sample_buffer* b, int root)
+{
+    if (!d || !c || !b) { SetError("null argument"); return -1; }
+    if (root < 0 || root >= c->nranks) { SetError("bad root %d", root); return -1; }
+    if ((int)b->nranks != c->nranks || (int)b->rank != c->rank) {
+        SetError("sample buffer partition %u/%u does not match communicator rank %d of %d", b->rank, b->nranks,
+                 c->rank, c->nranks);
+        return -1;
+    }
+    PT_HIP(hipSetDevice(d->id));
+    if (c->nranks == 1) return 0;
+    uint32_t bands = (b->height + 15) / 16;
+    ncclResult_t e = ncclGroupStart();
+    for (uint32_t band = 0; band < bands && e == ncclSuccess; band++) {
+        int owner = (int)(band % (uint32_t)c->nranks);
+        if (owner == root) continue;
+        uint32_t rows = std::min<uint32_t>(16u, b->height - band * 16u);
+        float* p = reinterpret_cast<float*>(b->accum + (size_t)band * 16 * b->width);
+        size_t count = (size_t)rows * b->width * 4;
+        if (c->rank == owner) e = ncclSend(p, count, ncclFloat32, root, c->comm, d->stream);
+        else if (c->rank == root) e = ncclRecv(p, count, ncclFloat32, owner, c->comm, d->stream);
+    }
+    ncclResult_t g = ncclGroupEnd();
+    if (e == ncclSuccess) e = g;
+    if (e != ncclSuccess) { SetError("band gather: %s", ncclGetErrorString(e)); return (int)e; }
     return 0;
 }
 

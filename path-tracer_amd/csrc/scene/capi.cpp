@@ -293,6 +293,28 @@ void ptsMeshVertices(pts_mesh* m, float* out)
 
 int ptsMaterialType(pts_material* m) { return m ? (int)reinterpret_cast<material*>(m)->Type : -1; }
 
+static entity* FindCamera(entity* e, uint32_t index)
+{
+    if (e->Type == ENTITY_TYPE_CAMERA && e->PackedCameraIndex == index) return e;
+    for (entity* c : e->Children)
+        if (entity* f = FindCamera(c, index)) return f;
+    return nullptr;
+}
+
+pts_entity* ptsFindCamera(pts_scene* s, uint32_t packed_index)
+{
+    entity* e = FindCamera(&S(s)->Root, packed_index);
+    if (!e) g_err = "no camera with packed index " + std::to_string(packed_index);
+    return reinterpret_cast<pts_entity*>(e);
+}
+
+void ptsSetCameraTransform(pts_scene* s, pts_entity* c, const float p[3], const float r[3])
+{
+    if (p) E(c)->Transform.Position = vec3(p[0], p[1], p[2]);
+    if (r) E(c)->Transform.Rotation = vec3(r[0], r[1], r[2]);
+    S(s)->DirtyFlags |= PT_SCENE_DIRTY_CAMERAS;
+}
+
 uint32_t ptsPackSceneData(pts_scene* s) { return PackSceneData(S(s)); }
 void ptsGetScenePacks(pts_scene* s, pt_scene_packs* out) { GetScenePacks(S(s), out); }
 void ptsMarkDirty(pts_scene* s, uint32_t flags) { S(s)->DirtyFlags |= flags; }

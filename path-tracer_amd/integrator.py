@@ -225,6 +225,12 @@ class BasicRenderer:
     def run(self, rounds: int = 1):
         _check(N.hip_lib().ptRunBasicRenderer(self.device.handle, self._h, int(rounds)), "ptRunBasicRenderer")
 
+    def stats(self):
+        """(rays traced, paths completed) since the last Reset (ptGetStats)."""
+        rays, samples = C.c_uint64(0), C.c_uint64(0)
+        _check(N.hip_lib().ptGetStats(self.device.handle, self._h, C.byref(rays), C.byref(samples)), "ptGetStats")
+        return int(rays.value), int(samples.value)
+
     def extend_stats(self) -> dict:
         """Traversal counters of the current rays (diagnostic, ptExtendStats)."""
         out = (C.c_uint64 * 14)()
@@ -342,6 +348,11 @@ class Comm:
     def reduce_sample_buffer(self, sample_buffer: SampleBuffer, root: int = 0):
         _check(N.hip_lib().ptCommReduceSampleBuffer(self.device.handle, self._h, sample_buffer.handle, root),
                "ptCommReduceSampleBuffer")
+
+    def gather_sample_buffer(self, sample_buffer: SampleBuffer, root: int = 0):
+        """Each rank's own bands, point-to-point to `root` (1/N of the reduce's traffic)."""
+        _check(N.hip_lib().ptCommGatherSampleBuffer(self.device.handle, self._h, sample_buffer.handle, root),
+               "ptCommGatherSampleBuffer")
 
     def close(self):
         if self._h:

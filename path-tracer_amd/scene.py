@@ -16,6 +16,9 @@ from . import _native as N
 ENTITY_CONTAINER, ENTITY_CAMERA, ENTITY_MESH_INSTANCE, ENTITY_PLANE, ENTITY_SPHERE, ENTITY_CUBE = 1, 2, 3, 4, 5, 6
 MATERIAL_BASIC_DIFFUSE, MATERIAL_BASIC_METAL, MATERIAL_BASIC_TRANSLUCENT, MATERIAL_OPENPBR = 0, 1, 2, 3
 TEXTURE_RAW, TEXTURE_REFLECTANCE_WITH_ALPHA, TEXTURE_RADIANCE = 0, 1, 2
+# SCENE_DIRTY_* (scene.hpp:323-333)
+(SCENE_DIRTY_GLOBALS, SCENE_DIRTY_TEXTURES, SCENE_DIRTY_MATERIALS, SCENE_DIRTY_SHAPES, SCENE_DIRTY_MESHES,
+ SCENE_DIRTY_CAMERAS, SCENE_DIRTY_SKYBOX_TEXTURE) = (1 << i for i in range(7))
 SCENE_DIRTY_ALL = 0xFFFFFFFF
 RENDER_FLAG_ACCUMULATE, RENDER_FLAG_SAMPLE_JITTER = 1, 2
 
@@ -119,6 +122,20 @@ class Scene:
 
     def set_camera_360(self, camera):
         N.scene_lib().ptsSetCamera360(self._h, camera)
+
+    def find_camera(self, packed_index: int = 0):
+        """The camera entity the last pack() placed at `packed_index`."""
+        L = N.scene_lib()
+        c = L.ptsFindCamera(self._h, int(packed_index))
+        if not c:
+            raise KeyError(L.ptsGetLastError().decode())
+        return c
+
+    def move_camera(self, camera, position=None, rotation=None):
+        """A camera move as the editor's fly controls make it
+        (application.cpp:52-66): only SCENE_DIRTY_CAMERAS is set, so the next
+        pack() re-packs the cameras alone."""
+        N.scene_lib().ptsSetCameraTransform(self._h, camera, _f3(position), _f3(rotation))
 
     def set_root(self, scatter_rate=0.0, skybox_brightness=1.0, skybox_sampling_probability=0.0, skybox=None):
         N.scene_lib().ptsSetRootParameters(self._h, scatter_rate, skybox_brightness, skybox_sampling_probability, skybox)

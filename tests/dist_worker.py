@@ -1,10 +1,15 @@
-"""Rank program for tests/test_distributed.py, launched exactly like bench.py
+"""Rank program for the multi-process tests, launched exactly like bench.py
 (python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1).
 
-Each rank renders its 16-row pixel bands with the CPU
-oracle, then the float4 accumulators are summed to rank 0 with a gloo
-reduce — the CPU stand-in for ptCommReduceSampleBuffer's ncclReduce — and
-rank 0 writes the reduced frame plus the max-over-ranks wall time.
+Each rank renders its 16-row pixel bands over two
+progressive frames (Reset + Run(2) + Run(1), then one more Run(1)); after
+each frame the float4 accumulators are summed to rank 0 with a gloo reduce,
+the CPU stand-in for ptCommReduceSampleBuffer's ncclReduce: like it, each
+rank contributes only its own bands.  Rank 0 writes both reduced frames and
+the max-over-ranks wall time.
+
+PT_DIST_RENDERER=gpu renders with the product (libpathtracer.so, every rank
+on device 0, -m gpu tests); the default is the CPU oracle (the CPU suite).
 """
 from __future__ import annotations
 
@@ -29,23 +34,44 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     pt = conftest.load_package()
     scene = pt.Scene.config(cfg)
-    o = oracle_lib.OracleRenderer(scene.packs(), W, H, rank=rank, nranks=world, threads=2)
-    o.RenderFlags = 3
+    gpu = os.environ.get("PT_DIST_RENDERER") == "gpu"
+    if gpu:
+        dev = pt.Device(0)
+        ds = pt.DeviceScene(dev)
+        ds.update(scene)
+        sb = pt.SampleBuffer(dev, W, H)
+        r = pt.BasicRenderer(dev, ds, sb, rank=rank, nranks=world)
+        accum = sb.read
+    else:
+        r = oracle_lib.OracleRenderer(scene.packs(), W, H, rank=rank, nranks=world, threads=2)
+        accum = r.accum
+    r.RenderFlags = 3
+    owned = pt.owned_pixels(W, H, rank, world)
+    frames = []
     dist.barrier()
     t0 = time.perf_counter()
-    o.reset()
-    o.run(2)
-    o.run(1)
-    acc = torch.from_numpy(o.accum())
-    dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
+    r.reset()
+    r.run(2)
+    r.run(1)
+    for frame in range(2):
+        if frame:
+            r.run(1)
+        a = accum()
+        a[~owned] = 0.0
+        acc = torch.from_numpy(a)
+        dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
+        frames.append(acc.numpy().copy())
     dist.barrier()
     dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
     dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-    owned = torch.tensor([int(pt.owned_pixels(W, H, rank, world).sum())], dtype=torch.int64)
-    dist.all_reduce(owned, op=dist.ReduceOp.SUM)
+    n_owned = torch.tensor([int(owned.sum())], dtype=torch.int64)
+    dist.all_reduce(n_owned, op=dist.ReduceOp.SUM)
     if rank == 0:
-        np.savez(out_path, accum=acc.numpy(), seconds=dt.numpy(), owned=owned.numpy(), world=world)
-    o.close()
+        np.savez(out_path, accum=frames[0], accum2=frames[1], seconds=dt.numpy(), owned=n_owned.numpy(), world=world)
+    r.close()
+    if gpu:
+        for x in (sb, ds, dev):
+            x.close()
     scene.close()
     dist.destroy_process_group()
 

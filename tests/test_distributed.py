@@ -1,7 +1,9 @@
 """Multi-rank path on CPU: world_size-2 gloo run of the band-partitioned
-render + frame-end sum reduce (the RCCL path of bench.py / ptCommReduce-
-SampleBuffer, with the CPU oracle standing in for the GPU renderer).  The
-reduced frame must equal the single-rank render bit for bit."""
+render + frame-end sum reduce over two progressive frames (the flow of
+bench.py / ptCommReduceSampleBuffer, with the CPU oracle standing in for the
+GPU renderer here; tests/test_gpu_coverage.py runs the same worker with the
+product renderer on the GPU).  Both reduced frames must equal the
+single-rank render bit for bit."""
 from __future__ import annotations
 
 import os
@@ -42,9 +44,12 @@ def test_two_rank_band_render_reduces_to_full_frame(pt, tmp_path):
     o.run(2)
     o.run(1)
     full = o.accum()
+    o.run(1)
+    full2 = o.accum()
     o.close()
     s.close()
     assert np.array_equal(got["accum"].view(np.uint32), full.view(np.uint32))
+    assert np.array_equal(got["accum2"].view(np.uint32), full2.view(np.uint32))
 
 
 def test_band_ownership(pt):

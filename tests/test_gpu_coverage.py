@@ -1,0 +1,273 @@
+"""GPU parity of the renderer parameters and the callers' flows that
+test_gpu_parity.py does not exercise (all through libpathtracer.so, checked
+against the CPU oracle bit for bit):
+
+* C4 (3840x2160, BASELINE configs[3]) as the 1/8 pixel-band partitions the
+  8-GPU run gives ranks 0 and 7 (basic.glsl.inc:9-10: the reference itself
+  cannot hold this frame);
+* every RenderFlags combination (basic_scatter.glsl:15-18 no-jitter sample
+  position, :354-357 overwrite instead of accumulate) and Russian roulette
+  with PathTerminationProbability > 0 (:295-298);
+* OBJ materials left as OpenPBR, whose hits end the path with no
+  contribution (scene.glsl.inc:685-693);
+* the editor's camera move: PackSceneData re-packs only the cameras,
+  UpdateVulkanScene uploads only them, then Reset + Run(2) + Run(1)
+  (application.cpp:52-66,88-115);
+* ptGetStats and the RCCL frame-end reduce (idempotent over progressive
+  frames);
+* two processes rendering their bands with the product renderer and summing
+  over gloo (the CPU stand-in for the RCCL reduce; RCCL refuses two ranks on
+  one device), equal to the single-process frame.
+"""
+from __future__ import annotations
+
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle_lib
+from test_gpu_parity import compare_state, render_pair
+
+pytestmark = pytest.mark.gpu
+
+HERE = Path(__file__).resolve().parent
+
+
+@pytest.fixture(scope="module")
+def dev(pt):
+    if pt.device_count() < 1:
+        pytest.skip("no HIP device")
+    d = pt.Device(0)
+    yield d
+    d.close()
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+@pytest.mark.parametrize("rank", [0, 7])
+def test_c4_rank_of_8_partition_bit_exact(pt, dev, rank):
+    """One rank's share of the C4 frame: 3840x2160 split in 16-row bands over
+    8 ranks (1,036,800 slots each; rank 7 owns the ragged last band)."""
+    s = pt.Scene.config(4)
+    W, H = s.info.width, s.info.height
+    assert (W, H) == (3840, 2160)
+    gs, os_, ga, oa = render_pair(pt, dev, 4, W, H, [2, 1], rank=rank, nranks=8, scene=s)
+    owned = pt.owned_pixels(W, H, rank, 8)
+    assert owned.sum() == (1036800 if rank == 0 else 1036800 - 3840 * 8)
+    compare_state(gs, os_)
+    assert np.array_equal(bits(ga), bits(oa))
+    assert oa[owned][:, 3].sum() > 0 and not oa[~owned].any()
+    s.close()
+
+
+# (config, W, H, RenderFlags, PathTerminationProbability)
+PARAM_CASES = [
+    (1, 64, 64, 3, 0.1),     # roulette on, few terminations
+    (1, 64, 64, 3, 0.5),     # roulette on, most paths end by roulette
+    (1, 64, 64, 0, 0.0),     # no jitter (pixel centres), overwrite
+    (1, 64, 64, 1, 0.0),     # no jitter, accumulate
+    (1, 64, 64, 2, 0.0),     # jitter, overwrite
+    (2, 96, 96, 3, 0.5),     # sky + metal + glass with roulette
+    (5, 128, 64, 0, 0.3),    # mixed scene + medium, no jitter, overwrite, roulette
+    (5, 128, 64, 1, 0.1),
+    (3, 160, 90, 2, 0.2),    # mesh scene
+]
+
+
+@pytest.mark.parametrize("config,W,H,flags,p", PARAM_CASES)
+def test_render_flags_and_roulette_bit_exact(pt, dev, config, W, H, flags, p):
+    gs, os_, ga, oa = render_pair(pt, dev, config, W, H, [2, 1, 1], flags=flags, termination=p)
+    compare_state(gs, os_)
+    assert np.array_equal(bits(ga), bits(oa))
+    assert oa[..., 3].sum() > 0
+    if not flags & pt.RENDER_FLAG_ACCUMULATE:
+        # overwrite: a pixel holds its last completed sample only
+        assert oa[..., 3].max() == 1.0
+
+
+def test_openpbr_materials_end_paths(pt, dev, tmp_path):
+    """An imported OBJ keeps its OpenPBR materials (the reference's import,
+    scene.cpp:671-729): a path that hits them ends with no contribution
+    (scene.glsl.inc:685-693)."""
+    import test_ingestion as ti
+    path = ti.write_model(tmp_path)
+    s = pt.Scene.create()
+    e = s.instantiate_prefab(s.load_model_as_prefab(path, openpbr_as_diffuse=False))
+    s.set_transform(e, position=(0.2, 0.1, 0.4), rotation=(0.3, 0.2, 0.1), scale=(0.3, 0.3, 0.3))
+    s.pack()
+    mats = s.arrays()["materials"].reshape(-1, 32)[:, 0]
+    types = {int(mats[int(sh["MaterialIndex"])]) for sh in s.arrays()["shapes"]}
+    assert 3 in types                      # OpenPBR shapes present
+    gs, os_, ga, oa = render_pair(pt, dev, None, 64, 48, [2, 1, 1], scene=s)
+    compare_state(gs, os_)
+    assert np.array_equal(bits(ga), bits(oa))
+    assert oa[..., 3].sum() > 0
+    s.close()
+
+
+def test_camera_move_dirty_update_bit_exact(pt, dev):
+    """The application's camera move: only the cameras are re-packed and
+    uploaded, then Reset + Run(2) + Run(1) on the same renderer; bit-exact
+    against a fresh oracle on the updated packs at the same FrameIndex."""
+    s = pt.Scene.config(3)
+    W, H = 160, 90
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    sb = pt.SampleBuffer(dev, W, H)
+    r = pt.BasicRenderer(dev, ds, sb)
+    r.RenderFlags = 3
+    r.reset()
+    r.run(2)
+    r.run(1)
+    cam = s.find_camera(0)
+    before = s.arrays()["cameras"][0].copy()
+    s.move_camera(cam, position=(0.3, -1.2, 1.4), rotation=(1.45, 0.0, 0.35))
+    dirty = s.pack()
+    assert dirty == pt.SCENE_DIRTY_CAMERAS
+    assert not np.array_equal(s.arrays()["cameras"][0]["Transform"]["To"], before["Transform"]["To"])
+    ds.update(s, dirty)
+    frame = r.FrameIndex
+    r.reset()
+    r.run(2)
+    r.run(1)
+    o = oracle_lib.OracleRenderer(s.packs(), W, H)
+    o.RenderFlags = 3
+    o.FrameIndex = frame
+    o.reset()
+    o.run(2)
+    o.run(1)
+    dev.synchronize()
+    compare_state(r.read_state(), o.state())
+    assert np.array_equal(bits(sb.read()), bits(o.accum()))
+    o.close()
+    for x in (r, sb, ds):
+        x.close()
+    s.close()
+
+
+def test_get_stats_counts_rays_and_samples(pt, dev):
+    s = pt.Scene.config(2)
+    W, H, N = 96, 80, 2
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    sb = pt.SampleBuffer(dev, W, H)
+    r = pt.BasicRenderer(dev, ds, sb, rank=1, nranks=N)
+    r.RenderFlags = 3
+    r.reset()
+    assert r.stats() == (0, 0)
+    r.run(2)
+    r.run(3)
+    owned = int(pt.owned_pixels(W, H, 1, N).sum())
+    rays, samples = r.stats()
+    assert rays == 5 * owned
+    assert samples == int(sb.read()[..., 3].sum())      # ACCUMULATE: one alpha increment per sample
+    assert 0 < samples < rays
+    r.reset()
+    assert r.stats() == (0, 0)
+    for x in (r, sb, ds):
+        x.close()
+    s.close()
+
+
+def test_comm_reduce_is_idempotent_over_progressive_frames(pt, dev):
+    """ptCommReduceSampleBuffer on a one-rank RCCL communicator: rows outside
+    the renderer's bands never enter the sum, even when they hold stale totals
+    (the root's buffer after an earlier reduce)."""
+    s = pt.Scene.config(1)
+    W, H = 64, 80
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    sb = pt.SampleBuffer(dev, W, H)
+    r = pt.BasicRenderer(dev, ds, sb, rank=0, nranks=2)
+    o = oracle_lib.OracleRenderer(s.packs(), W, H, rank=0, nranks=2)
+    comm = pt.Comm(dev, 1, 0, pt.Comm.unique_id())
+    owned = pt.owned_pixels(W, H, 0, 2)
+    for x in (r, o):
+        x.RenderFlags = 3
+        x.reset()
+        x.run(2)
+    for frame in range(2):
+        a = sb.read()
+        a[~owned] = 7.0 + frame                      # stale totals in the other rank's bands
+        sb.write(a)
+        comm.reduce_sample_buffer(sb, 0)
+        dev.synchronize()
+        assert np.array_equal(bits(sb.read()), bits(o.accum())), f"frame {frame}"
+        for x in (r, o):
+            x.run(1)
+    comm.close()
+    o.close()
+    for x in (r, sb, ds):
+        x.close()
+    s.close()
+
+
+def free_port():
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def test_two_process_band_render_equals_single_process(pt, dev, tmp_path):
+    """Two ranks (processes) on this GPU, each rendering its bands of a C5
+    frame with the product renderer over two progressive frames, summed to
+    rank 0 over gloo; equal bit for bit to this process's 1-rank frames."""
+    cfg, W, H = 5, 128, 80
+    out = tmp_path / "reduced.npz"
+    env = dict(os.environ, OMP_NUM_THREADS="2", HSA_ENABLE_IPC_MODE_LEGACY="0", PT_DIST_RENDERER="gpu")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           str(HERE / "dist_worker.py"), str(out), str(cfg), str(W), str(H)]
+    res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-3000:]
+    got = np.load(out)
+    s = pt.Scene.config(cfg)
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    sb = pt.SampleBuffer(dev, W, H)
+    r = pt.BasicRenderer(dev, ds, sb)
+    r.RenderFlags = 3
+    r.reset()
+    r.run(2)
+    r.run(1)
+    frame0 = sb.read()
+    r.run(1)
+    frame1 = sb.read()
+    assert int(got["owned"][0]) == W * H
+    assert np.array_equal(bits(got["accum"]), bits(frame0))
+    assert np.array_equal(bits(got["accum2"]), bits(frame1))
+    for x in (r, sb, ds):
+        x.close()
+    s.close()
+
+
+def test_comm_gather_single_rank_and_partition_check(pt, dev):
+    """ptCommGatherSampleBuffer: a one-rank communicator has nothing to move
+    (the buffer is unchanged); a buffer partitioned for another rank count
+    is rejected before any RCCL call."""
+    s = pt.Scene.config(1)
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    sb = pt.SampleBuffer(dev, 48, 40)
+    r = pt.BasicRenderer(dev, ds, sb)
+    r.RenderFlags = 3
+    r.reset()
+    r.run(2)
+    comm = pt.Comm(dev, 1, 0, pt.Comm.unique_id())
+    before = sb.read()
+    comm.gather_sample_buffer(sb, 0)
+    assert np.array_equal(bits(sb.read()), bits(before))
+    r2 = pt.BasicRenderer(dev, ds, sb, rank=1, nranks=2)   # the buffer is now partitioned 1 of 2
+    with pytest.raises(pt.PathTracerError):
+        comm.gather_sample_buffer(sb, 0)
+    comm.close()
+    for x in (r2, r, sb, ds):
+        x.close()
+    s.close()

@@ -137,15 +137,19 @@ def test_deep_stack_spills_bit_exact(pt, dev, tmp_path):
     s.close()
 
 
-def render_pair(pt, dev, config, W, H, schedule, camera=0):
-    s = scene_for(pt, config)
+def render_pair(pt, dev, config, W, H, schedule, camera=0, flags=3, termination=0.0, rank=0, nranks=1,
+                scene=None):
+    """The same Reset + Run(schedule...) on the HIP renderer and the oracle:
+    (GPU state, oracle state, GPU accumulator, oracle accumulator)."""
+    s = scene if scene is not None else scene_for(pt, config)
     ds = pt.DeviceScene(dev)
     ds.update(s)
     sb = pt.SampleBuffer(dev, W, H)
-    r = pt.BasicRenderer(dev, ds, sb)
-    o = oracle_lib.OracleRenderer(s.packs(), W, H)
+    r = pt.BasicRenderer(dev, ds, sb, rank=rank, nranks=nranks)
+    o = oracle_lib.OracleRenderer(s.packs(), W, H, rank=rank, nranks=nranks)
     for x in (r, o):
-        x.RenderFlags = pt.RENDER_FLAG_ACCUMULATE | pt.RENDER_FLAG_SAMPLE_JITTER
+        x.RenderFlags = flags
+        x.PathTerminationProbability = termination
         x.CameraIndex = camera
         x.reset()
         for rounds in schedule:
@@ -191,13 +195,15 @@ def test_image_rel_l2(pt, dev, config, W, H):
     (1, 256, 256, [2] + [1] * 14, 0),    # C1 at its full 256x256, 16 spp
     (2, 1024, 1024, [2, 1], 0),          # C2 at its full 1024x1024
     (3, 1920, 1080, [2] + [1] * 6, 0),   # C3 (the bench workload) at its full 1920x1080, 8 rounds
-    (5, 1920, 1080, [2, 1], 0),          # C5 thin-lens camera
-    (5, 1920, 1080, [2, 1], 1),          # C5 360 camera
+    (5, 2048, 1024, [2, 1], 0),          # C5 at its declared 2048x1024, thin-lens camera
+    (5, 2048, 1024, [2, 1], 1),          # C5 360 camera
 ])
 def test_full_size_bit_exact(pt, dev, config, W, H, schedule, camera):
-    """BASELINE.json's resolutions: every slot's state and every accumulated
-    pixel bit-exact, over the tile / TileOrder / ShadeOrder layout of a full
-    frame (8100 tiles at 1080p, ragged last tile row)."""
+    """The configs' declared resolutions (configs.cpp): every
+    slot's state and every accumulated pixel bit-exact, over the tile /
+    TileOrder / ShadeOrder layout of a full frame (8100 tiles at 1080p, ragged
+    last tile row).  C4's 3840x2160 frame is covered per rank in
+    test_gpu_coverage.py."""
     gs, os_, ga, oa = render_pair(pt, dev, config, W, H, schedule, camera=camera)
     compare_state(gs, os_)
     assert oa[..., 3].sum() > 0
