@@ -53,14 +53,14 @@ def bits(a):
 
 @pytest.mark.parametrize("rank", [0, 7])
 def test_c4_rank_of_8_partition_bit_exact(pt, dev, rank):
-    """One rank's share of the C4 frame: 3840x2160 split in 16-row bands over
-    8 ranks (1,036,800 slots each; rank 7 owns the ragged last band)."""
+    """One rank's share of the C4 frame: 3840x2160 = 135 bands of 16 rows over
+    8 ranks (ranks 0-6 own 17 bands = 1,044,480 slots, rank 7 owns 16)."""
     s = pt.Scene.config(4)
     W, H = s.info.width, s.info.height
     assert (W, H) == (3840, 2160)
     gs, os_, ga, oa = render_pair(pt, dev, 4, W, H, [2, 1], rank=rank, nranks=8, scene=s)
     owned = pt.owned_pixels(W, H, rank, 8)
-    assert owned.sum() == (1036800 if rank == 0 else 1036800 - 3840 * 8)
+    assert owned.sum() == 3840 * 16 * (17 if rank == 0 else 16)
     compare_state(gs, os_)
     assert np.array_equal(bits(ga), bits(oa))
     assert oa[owned][:, 3].sum() > 0 and not oa[~owned].any()
