@@ -188,6 +188,10 @@ pt_basic_renderer_params* ptBasicRendererParams(pt_basic_renderer* renderer);
 int                ptResetBasicRenderer(pt_device* device, pt_basic_renderer* renderer);
 int                ptRunBasicRenderer(pt_device* device, pt_basic_renderer* renderer, uint32_t rounds);
 uint32_t           ptBasicRendererSlotCount(pt_basic_renderer* renderer);
+/* Independent tile groups a Run advances on their own streams (1 for a
+ * renderer that fills the GPU; more for small partitions);
+ * each kernel launch covers one group's tiles. */
+uint32_t           ptBasicRendererRunGroups(pt_basic_renderer* renderer);
 /* Work done since the last Reset: rays traced (one per owned pixel per round)
  * and paths completed (accumulator sample increments, basic_scatter.glsl:
  * 350-359).  Either pointer may be NULL.  Synchronises the device stream. */

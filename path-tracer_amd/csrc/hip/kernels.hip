@@ -731,6 +731,7 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
     uint32_t tile = blockIdx.x;
     uint64_t t0 = 0;
     if constexpr (std::is_same<Src, ray_source_slots>::value) {
+        tile += src.L.tile_base;
         if (src.L.order) {
             tile = src.L.order[blockIdx.x];
             t0 = __builtin_amdgcn_s_memtime();
@@ -753,8 +754,10 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
 // wave's time, descending, by a one-block counting sort over 512 log-spaced
 // buckets (16 per octave).  Any order gives the same results; only the
 // kernel's tail changes.
-__global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, uint32_t* order, uint32_t tiles)
+__global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, uint32_t* order, uint32_t base,
+                                                          uint32_t tiles)
 {
+    cost += 4 * (size_t)base;
     __shared__ uint32_t count[512];
     for (uint32_t i = threadIdx.x; i < 512; i += 1024) count[i] = 0;
     __syncthreads();
@@ -773,7 +776,7 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, 
         for (uint32_t i = 0; i < 512; i++) { uint32_t c = count[i]; count[i] = sum; sum += c; }
     }
     __syncthreads();
-    for (uint32_t t = threadIdx.x; t < tiles; t += 1024) order[atomicAdd(&count[key(t)], 1u)] = t;
+    for (uint32_t t = threadIdx.x; t < tiles; t += 1024) order[atomicAdd(&count[key(t)], 1u)] = base + t;
 }
 
 __global__ __launch_bounds__(256) void zero_unowned_kernel(float4* accum, uint32_t width, uint32_t height,
@@ -873,7 +876,7 @@ __global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MIN
     // state is read and written by slot (gathers within the tile's records).
     // Tiles in extend's longest-first order too: tiles with long traversals
     // also shade more hits (C5 shade -3 %).
-    const uint32_t tile = L.order ? L.order[blockIdx.x] : blockIdx.x;
+    const uint32_t tile = L.order ? L.order[blockIdx.x] : L.tile_base + blockIdx.x;
     const uint32_t base = tile * 256;
 #if PT_SHADE_ORDER
     const uint64_t* om = L.outcome + (size_t)tile * (4 * PT_OUTCOME_CLASSES);
@@ -1038,21 +1041,24 @@ uint32_t pt_extend_stack_cap()
 }
 
 template <class Src, int W, int CAP, class E>
-static void LaunchExtendE(const ptd::dscene& S, const Src& src, uint32_t n, uint32_t* spill, uint32_t pad,
-                          hipStream_t st)
+static void LaunchExtendE(const ptd::dscene& S, const Src& src, uint32_t n, uint32_t blocks, uint32_t* spill,
+                          uint32_t pad, hipStream_t st)
 {
     if (spill)
-        hipLaunchKernelGGL((ptd::extend_kernel<Src, true, W, CAP, E>), dim3(Blocks(n)), dim3(256), pad, st, S, src, n,
+        hipLaunchKernelGGL((ptd::extend_kernel<Src, true, W, CAP, E>), dim3(blocks), dim3(256), pad, st, S, src, n,
                            spill, n);
     else
-        hipLaunchKernelGGL((ptd::extend_kernel<Src, false, W, CAP, E>), dim3(Blocks(n)), dim3(256), pad, st, S, src, n,
+        hipLaunchKernelGGL((ptd::extend_kernel<Src, false, W, CAP, E>), dim3(blocks), dim3(256), pad, st, S, src, n,
                            spill, n);
 }
 
+// n: rays (the spill stride and the bound of the ray index); blocks: the
+// launch's 256-ray blocks (a run group's tiles for the slot renderer).
 template <class Src>
-static hipError_t LaunchExtend(const ptd::dscene& S, const Src& src, uint32_t n, uint32_t* spill, hipStream_t st)
+static hipError_t LaunchExtend(const ptd::dscene& S, const Src& src, uint32_t n, uint32_t blocks, uint32_t* spill,
+                               hipStream_t st)
 {
-    if (n == 0) return hipSuccess;
+    if (n == 0 || blocks == 0) return hipSuccess;
     // PT_EXTEND_LDS_PAD: extra (unused) dynamic LDS per block, an occupancy cap
     // for experiments (e.g. 12288 -> 5 blocks per CU).
     static const uint32_t pad = []() {
@@ -1062,8 +1068,8 @@ static hipError_t LaunchExtend(const ptd::dscene& S, const Src& src, uint32_t n,
     switch (pt_extend_variant()) {
 #define X(id, w, cap)                                                                                           \
     case id:                                                                                                   \
-        if (S.stack16) LaunchExtendE<Src, w, cap, uint16_t>(S, src, n, spill, pad, st);                         \
-        else LaunchExtendE<Src, w, cap, uint32_t>(S, src, n, spill, pad, st);                                   \
+        if (S.stack16) LaunchExtendE<Src, w, cap, uint16_t>(S, src, n, blocks, spill, pad, st);                 \
+        else LaunchExtendE<Src, w, cap, uint32_t>(S, src, n, blocks, spill, pad, st);                           \
         break;
         PT_EXTEND_VARIANTS(X)
 #undef X
@@ -1103,8 +1109,9 @@ hipError_t pt_launch_extend_stats(const ptd::dscene& S, const ptd::dslots& L, co
 
 hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st)
 {
-    if (!L.order || L.n == 0) return hipSuccess;
-    hipLaunchKernelGGL(ptd::tile_order_kernel, dim3(1), dim3(1024), 0, st, L.tilecost, L.order, L.n / 256);
+    if (!L.order || L.tile_count == 0) return hipSuccess;
+    hipLaunchKernelGGL(ptd::tile_order_kernel, dim3(1), dim3(1024), 0, st, L.tilecost, L.order, L.tile_base,
+                       L.tile_count);
     return hipGetLastError();
 }
 
@@ -1120,7 +1127,7 @@ hipError_t pt_launch_zero_unowned(float4* accum, uint32_t width, uint32_t height
 hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* spill,
                             hipStream_t st)
 {
-    return LaunchExtend(S, ptd::ray_source_slots{L, F}, L.n, spill, st);
+    return LaunchExtend(S, ptd::ray_source_slots{L, F}, L.n, L.tile_count, spill, st);
 }
 
 // Shade instantiations by material-type mask: the smallest superset of the
@@ -1135,17 +1142,17 @@ uint32_t pt_shade_mats(uint32_t scene_mats)
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
                            uint32_t scene_mats, hipStream_t st)
 {
-    if (L.n == 0) return hipSuccess;
+    if (L.n == 0 || L.tile_count == 0) return hipSuccess;
     switch (pt_shade_mats(scene_mats)) {
     case PT_MATS_DIFFUSE:
-        hipLaunchKernelGGL(ptd::shade_kernel<PT_MATS_DIFFUSE>, dim3(Blocks(L.n)), dim3(256), 0, st, S, L, F, P);
+        hipLaunchKernelGGL(ptd::shade_kernel<PT_MATS_DIFFUSE>, dim3(L.tile_count), dim3(256), 0, st, S, L, F, P);
         break;
     case PT_MATS_DIFFUSE | PT_MATS_METAL:
-        hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_DIFFUSE | PT_MATS_METAL>), dim3(Blocks(L.n)), dim3(256), 0, st,
+        hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_DIFFUSE | PT_MATS_METAL>), dim3(L.tile_count), dim3(256), 0, st,
                            S, L, F, P);
         break;
     default:
-        hipLaunchKernelGGL(ptd::shade_kernel<PT_MATS_ALL>, dim3(Blocks(L.n)), dim3(256), 0, st, S, L, F, P);
+        hipLaunchKernelGGL(ptd::shade_kernel<PT_MATS_ALL>, dim3(L.tile_count), dim3(256), 0, st, S, L, F, P);
         break;
     }
     return hipGetLastError();
@@ -1167,7 +1174,7 @@ hipError_t pt_launch_trace_rays(const ptd::dscene& S, uint32_t n, const float* o
                                 const float* dur, float4* hit, float2* hc, float4* rec, float2* uv, uint32_t* spill,
                                 hipStream_t st)
 {
-    hipError_t e = LaunchExtend(S, ptd::ray_source_arrays{origins, vel, dur, hit, hc}, n, spill, st);
+    hipError_t e = LaunchExtend(S, ptd::ray_source_arrays{origins, vel, dur, hit, hc}, n, Blocks(n), spill, st);
     if (e != hipSuccess) return e;
     return pt_launch_finalize(S, n, hit, hc, rec, uv, st);
 }

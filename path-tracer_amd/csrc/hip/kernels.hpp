@@ -39,6 +39,10 @@ struct dslots {
     uint32_t* done;     // per wave of 64 slots: paths completed by shade since the last Reset (ptGetStats)
     uint32_t* spill;    // traversal stack spill: (needed - LDS capacity) rows x n
     uint32_t n;
+    // The launch's tile range (a run group, runtime.hip): tiles
+    // [tile_base, tile_base + tile_count); `order` then points at the group's
+    // segment of the block -> tile map.
+    uint32_t tile_base, tile_count;
 };
 
 struct dframe {

@@ -71,7 +71,7 @@ struct dbuf {
     }
 };
 
-struct event_pair { hipEvent_t a, b; int kernel; };
+struct event_pair { hipEvent_t a, b; int kernel; hipStream_t stream; };
 
 }  // namespace
 
@@ -144,6 +144,15 @@ struct pt_basic_renderer {
     dbuf<uint32_t> tilecost, order;     // longest-first tile order (extend -> tile_order -> extend)
     uint64_t order_tick = 0;            // rounds since creation (tile-order re-sort period)
     dbuf<uint32_t> done;                // per wave: completed paths since the last Reset (ptGetStats)
+    // Run groups: the tiles split into `groups` contiguous ranges, each
+    // advanced round by round on its own stream, so a group's next round
+    // starts while another group's extend is still draining its longest
+    // tiles (a partition too small to fill the GPU: strong scaling).
+    static constexpr uint32_t MAX_GROUPS = 4;
+    uint32_t groups = 1;
+    hipStream_t gstream[MAX_GROUPS] = {};
+    hipEvent_t gevent[MAX_GROUPS] = {};
+    hipEvent_t fork = nullptr;
     uint64_t pixels = 0;                // image pixels owned (valid slots)
     uint64_t rays = 0;                  // rays traced since the last Reset
     dbuf<uint32_t> spill;
@@ -157,7 +166,7 @@ struct pt_comm {
 
 namespace {
 
-int BeginTimed(pt_device* dev, int kernel, event_pair& ep, bool sampled = true)
+int BeginTimed(pt_device* dev, int kernel, event_pair& ep, bool sampled = true, hipStream_t stream = nullptr)
 {
     ep.kernel = -1;
     if (!dev->profiling || !sampled) return 0;
@@ -167,14 +176,15 @@ int BeginTimed(pt_device* dev, int kernel, event_pair& ep, bool sampled = true)
         PT_HIP(hipEventCreate(&ep.b));
     }
     ep.kernel = kernel;
-    PT_HIP(hipEventRecord(ep.a, dev->stream));
+    ep.stream = stream ? stream : dev->stream;
+    PT_HIP(hipEventRecord(ep.a, ep.stream));
     return 0;
 }
 
 int EndTimed(pt_device* dev, event_pair& ep)
 {
     if (!dev->profiling || ep.kernel < 0) return 0;
-    PT_HIP(hipEventRecord(ep.b, dev->stream));
+    PT_HIP(hipEventRecord(ep.b, ep.stream));
     dev->pending.push_back(ep);
     return 0;
 }
@@ -663,6 +673,21 @@ static uint32_t TileOrderPeriod()
     return v;
 }
 
+// Run groups for a renderer of `tiles` 256-slot tiles: PT_RUN_GROUPS (an
+// experiment knob), else 1.  Measured on the rank-0-of-N partitions of C3
+// (tools/rehearse_scaling.py): 2-4 groups on separate streams
+// are slower at every N (N=8: 0.156 / 0.262 / 0.267 vs 0.131 ms per round),
+// since each group's extend still lasts as long as its longest tile and the
+// concurrent launches mostly serialise.
+static uint32_t RunGroups(uint32_t tiles, uint32_t cus)
+{
+    (void)cus;
+    const char* e = getenv("PT_RUN_GROUPS");
+    uint32_t g = e ? (uint32_t)std::max(1, atoi(e)) : 1u;
+    g = std::min<uint32_t>(g, pt_basic_renderer::MAX_GROUPS);
+    return std::max<uint32_t>(1u, std::min<uint32_t>(g, tiles));
+}
+
 // PT_TILE_ORDER=0: extend dispatches tiles in their natural order.
 static bool TileOrderEnabled()
 {
@@ -737,6 +762,18 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     r->slots.done = r->done.ptr;
     r->slots.spill = nullptr;
     r->slots.n = ns;
+    r->slots.tile_base = 0;
+    r->slots.tile_count = ns / 256;
+    r->groups = RunGroups(ns / 256, d->cu_count);
+    for (uint32_t g = 0; g < r->groups && r->groups > 1 && ok; g++)
+        ok = hipStreamCreateWithFlags(&r->gstream[g], hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&r->gevent[g], hipEventDisableTiming) == hipSuccess;
+    if (ok && r->groups > 1) ok = hipEventCreateWithFlags(&r->fork, hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+        SetError("renderer stream creation failed");
+        ptDestroyBasicRenderer(d, r);
+        return nullptr;
+    }
     for (uint32_t band = rank; band < bands; band += nranks)
         r->pixels += (uint64_t)b->width * std::min<uint32_t>(16u, b->height - band * 16u);
     b->rank = rank;
@@ -758,6 +795,11 @@ void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
     r->tilecost.release(); r->order.release();
     r->done.release();
     r->spill.release();
+    for (uint32_t g = 0; g < pt_basic_renderer::MAX_GROUPS; g++) {
+        if (r->gstream[g]) (void)hipStreamDestroy(r->gstream[g]);
+        if (r->gevent[g]) (void)hipEventDestroy(r->gevent[g]);
+    }
+    if (r->fork) (void)hipEventDestroy(r->fork);
     delete r;
 }
 
@@ -790,21 +832,48 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
     ptd::dparams P = Params(r, r->params.FrameIndex);
     ptd::dframe F = Frame(r);
     bool sampled = d->profiling && (d->run_tick++ % d->profile_period) == 0;
+    const uint32_t G = r->groups, tiles = r->slots.n / 256;
+    // Group g: tiles [tiles*g/G, tiles*(g+1)/G) on its own stream, forked from
+    // and joined back into the device stream (ordering with Reset, scene
+    // updates and reads is that of one stream).
+    ptd::dslots gs[pt_basic_renderer::MAX_GROUPS];
+    hipStream_t st[pt_basic_renderer::MAX_GROUPS];
+    for (uint32_t g = 0; g < G; g++) {
+        gs[g] = r->slots;
+        gs[g].tile_base = (uint32_t)((uint64_t)tiles * g / G);
+        gs[g].tile_count = (uint32_t)((uint64_t)tiles * (g + 1) / G) - gs[g].tile_base;
+        if (gs[g].order) gs[g].order += gs[g].tile_base;
+        st[g] = G > 1 ? r->gstream[g] : d->stream;
+    }
+    if (G > 1) {
+        PT_HIP(hipEventRecord(r->fork, d->stream));
+        for (uint32_t g = 0; g < G; g++) PT_HIP(hipStreamWaitEvent(st[g], r->fork, 0));
+    }
     for (uint32_t i = 0; i < rounds; i++) {
-        event_pair ep{};
-        if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled)) return e;
-        PT_HIP(pt_launch_extend(r->scene->d, r->slots, F, r->slots.spill, d->stream));
-        if (int e = EndTimed(d, ep)) return e;
-        if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled)) return e;
-        PT_HIP(pt_launch_shade(r->scene->d, r->slots, F, P, r->scene->mats, d->stream));
-        if (int e = EndTimed(d, ep)) return e;
         // Tiles keep their relative cost for many rounds: re-sort every
-        // TileOrderPeriod() rounds (the sort is one small launch).
-        if (r->slots.order && (r->order_tick++ % TileOrderPeriod()) == 0) PT_HIP(pt_launch_tile_order(r->slots, d->stream));
+        // TileOrderPeriod() rounds (the sort is one small launch per group).
+        bool sort = r->slots.order && (r->order_tick++ % TileOrderPeriod()) == 0;
+        for (uint32_t g = 0; g < G; g++) {
+            event_pair ep{};
+            if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled, st[g])) return e;
+            PT_HIP(pt_launch_extend(r->scene->d, gs[g], F, r->slots.spill, st[g]));
+            if (int e = EndTimed(d, ep)) return e;
+            if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled, st[g])) return e;
+            PT_HIP(pt_launch_shade(r->scene->d, gs[g], F, P, r->scene->mats, st[g]));
+            if (int e = EndTimed(d, ep)) return e;
+            if (sort) PT_HIP(pt_launch_tile_order(gs[g], st[g]));
+        }
         r->rays += r->pixels;
     }
+    if (G > 1)
+        for (uint32_t g = 0; g < G; g++) {
+            PT_HIP(hipEventRecord(r->gevent[g], st[g]));
+            PT_HIP(hipStreamWaitEvent(d->stream, r->gevent[g], 0));
+        }
     return 0;
 }
+
+uint32_t ptBasicRendererRunGroups(pt_basic_renderer* r) { return r ? r->groups : 0; }
 
 // Counters of the work done since the last Reset: rays traced (every owned
 // pixel's slot traces one ray per round, K3) and paths completed (the

@@ -219,6 +219,11 @@ class BasicRenderer:
     def slot_count(self) -> int:
         return int(N.hip_lib().ptBasicRendererSlotCount(self._h))
 
+    @property
+    def run_groups(self) -> int:
+        """Tile groups advanced on separate streams (ptBasicRendererRunGroups)."""
+        return int(N.hip_lib().ptBasicRendererRunGroups(self._h))
+
     def reset(self):
         _check(N.hip_lib().ptResetBasicRenderer(self.device.handle, self._h), "ptResetBasicRenderer")
 

@@ -14,6 +14,7 @@ from __future__ import annotations
 import argparse
 import importlib.util
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -38,6 +39,7 @@ def main():
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--configs", default="3,4")
     ap.add_argument("--ns", default="1,2,4,8")
+    ap.add_argument("--groups", default="", help="comma list of PT_RUN_GROUPS values to try (default: the runtime's choice)")
     args = ap.parse_args()
     pt = load_package()
     dev = pt.Device(0)
@@ -47,7 +49,11 @@ def main():
         W, H = scene.info.width, scene.info.height
         ds = pt.DeviceScene(dev)
         ds.update(scene)
-        for n in [int(x) for x in args.ns.split(",")]:
+        for n, groups in [(int(x), g) for x in args.ns.split(",") for g in (args.groups.split(",") if args.groups else [None])]:
+            if groups is None:
+                os.environ.pop("PT_RUN_GROUPS", None)
+            else:
+                os.environ["PT_RUN_GROUPS"] = groups
             sb = pt.SampleBuffer(dev, W, H)
             r = pt.BasicRenderer(dev, ds, sb, rank=0, nranks=n)
             r.RenderFlags = scene.info.render_flags
@@ -71,7 +77,7 @@ def main():
             step_ms = dt / args.steps * 1e3
             row = {
                 "config": cfg, "frame": f"{W}x{H}", "n_gpus": n, "rank0_pixels": owned,
-                "rank0_tiles": r.slot_count // 256,
+                "rank0_tiles": r.slot_count // 256, "run_groups": r.run_groups,
                 "rank0_ms_per_step": round(step_ms, 4),
                 "rank0_mrays_per_s": round((rays1 - rays0) / dt / 1e6, 1),
                 "extend_ms": round(me / max(ne, 1), 4), "shade_ms": round(ms / max(ns_, 1), 4),
@@ -83,7 +89,10 @@ def main():
             sb.close()
         ds.close()
         scene.close()
-    base = {r["config"]: r["predicted_frame_mrays_per_s"] for r in rows if r["n_gpus"] == 1}
+    base = {}
+    for r in rows:
+        if r["n_gpus"] == 1:
+            base[r["config"]] = max(base.get(r["config"], 0), r["predicted_frame_mrays_per_s"])
     for r in rows:
         b = base.get(r["config"])
         if b:
