@@ -13,7 +13,7 @@
 // Slot s covers pixel (tx*16 + s%16, band*16 + (s%256)/16) of the tile
 // t = s/256, so a renderer can own an arbitrary set of 16-row bands.
 //
-// Ray order (TileOrder): the path arrays (thr, prob, smp, act) are indexed by
+// Ray order (TileOrder): the path arrays (thr, prob, lam, act) are indexed by
 // slot, the ray and hit arrays by POSITION within the same tile.  Whenever a
 // block of 256 slots (one tile) emits its rays, it sorts them by direction
 // octant with a block counting sort and stores slot s's ray at position
@@ -320,12 +320,21 @@ struct path {
     uint32_t Active[4];
 };
 
-PT_DEV void StorePathVertex(const dslots& L, uint32_t s, const path& P)
+// Path record (basic.glsl.inc:159-198 StorePathVertex) minus Sample: Scatter
+// adds to Sample only on escape, and the escape zeroes Probability, which
+// ends the path in the same shade (its Sample goes to the accumulator and a
+// new path starts with Sample = 0).  So every path alive between rounds has
+// Sample == 0 and only lambda0 is stored (4 bytes instead of 16); the state
+// readback reports the zero.
+// `act_none`: the slot's stored active-shape stack is already empty (all
+// four entries NONE), as a new path's is, so its 8-byte record is not
+// rewritten (a partial-line store for every completed path otherwise).
+PT_DEV void StorePathVertex(const dslots& L, uint32_t s, const path& P, bool act_none = false)
 {
     L.thr[s] = make_float4(P.Throughput.x, P.Throughput.y, P.Throughput.z, P.Throughput.w);
     L.prob[s] = make_float4(P.Probability.x, P.Probability.y, P.Probability.z, P.Probability.w);
-    L.smp[s] = make_float4(P.Sample.x, P.Sample.y, P.Sample.z, P.Lambda0);
-    L.act[s] = make_uint2((P.Active[1] << 16) | P.Active[0], (P.Active[3] << 16) | P.Active[2]);
+    L.lam[s] = P.Lambda0;
+    if (!act_none) L.act[s] = make_uint2((P.Active[1] << 16) | P.Active[0], (P.Active[3] << 16) | P.Active[2]);
 }
 
 // Position of the k-th set bit (k < popcount) of a 64-bit word: a 6-step
@@ -433,7 +442,7 @@ PT_DEV void TileOrderStoreRay(const dslots& L, uint32_t s, bool valid, pt3 O, pt
 
 // GenerateNewPath (basic_scatter.glsl:7-42) + GenerateCameraRay (scene.glsl.inc:613-655)
 PT_DEV void GenerateNewPath(const dscene& S, const dslots& L, const dframe& F, const dparams& Pm, rng& G, uint32_t s,
-                            uint32_t x, uint32_t y, pt3& RO, pt3& RV)
+                            uint32_t x, uint32_t y, pt3& RO, pt3& RV, bool act_none = false)
 {
     float SPx = (float)x, SPy = (float)y;
     if (Pm.render_flags & PT_RENDER_FLAG_SAMPLE_JITTER) {
@@ -476,7 +485,7 @@ PT_DEV void GenerateNewPath(const dscene& S, const dslots& L, const dframe& F, c
     P.Probability = v4s(1.0f);
     P.Sample = v3s(0.0f);
     P.Active[0] = P.Active[1] = P.Active[2] = P.Active[3] = SHAPE_INDEX_NONE;
-    StorePathVertex(L, s, P);
+    StorePathVertex(L, s, P, act_none);
 }
 
 // Scatter (basic_scatter.glsl:114-310).  Returns true if an extension ray was
@@ -779,6 +788,21 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, 
     for (uint32_t t = threadIdx.x; t < tiles; t += 1024) order[atomicAdd(&count[key(t)], 1u)] = base + t;
 }
 
+// Row-major packed atlas -> the device's 4x2-texel block layout (AtlasIndex):
+// one thread per destination texel, so the stores are contiguous.
+__global__ __launch_bounds__(256) void atlas_tile_kernel(const float4* src, float4* dst, uint32_t w, uint32_t h,
+                                                         uint64_t texels)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < texels; i += (uint64_t)gridDim.x * 256) {
+        uint64_t plane = (uint64_t)w * h;
+        uint64_t layer = i / plane, r = i - layer * plane;
+        uint32_t blk = (uint32_t)(r >> 3), in = (uint32_t)(r & 7u);
+        uint32_t by = blk / (w >> 2), bx = blk - by * (w >> 2);
+        uint32_t x = bx * 4 + (in & 3u), y = by * 2 + (in >> 2);
+        dst[i] = src[layer * plane + (uint64_t)y * w + x];
+    }
+}
+
 __global__ __launch_bounds__(256) void zero_unowned_kernel(float4* accum, uint32_t width, uint32_t height,
                                                            uint32_t rank, uint32_t nranks)
 {
@@ -896,12 +920,12 @@ __global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MIN
 
         // LoadPath (basic.glsl.inc:159-198)
         path P;
-        float4 thr = L.thr[s], prob = L.prob[s], smp = L.smp[s];
+        float4 thr = L.thr[s], prob = L.prob[s];
         uint2 act = L.act[s];
         P.Throughput = v4(thr.x, thr.y, thr.z, thr.w);
         P.Probability = v4(prob.x, prob.y, prob.z, prob.w);
-        P.Sample = v3(smp.x, smp.y, smp.z);
-        P.Lambda0 = smp.w;
+        P.Sample = v3s(0.0f);          // always 0 between rounds (StorePathVertex)
+        P.Lambda0 = L.lam[s];
         P.Active[0] = act.x & 0xFFFF; P.Active[1] = act.x >> 16;
         P.Active[2] = act.y & 0xFFFF; P.Active[3] = act.y >> 16;
         for (int I = 0; I < 4; I++)
@@ -934,7 +958,7 @@ __global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MIN
 
         if (Scatter<MATS>(S, G, Pm.termination_probability, P, O, V, HitShape, HitMaterial, HitTime, PN, PTg, UV)) {
             // StorePathVertex of a continuing path: Scatter changes Sample only
-            // on escape (which terminates the path) and never Lambda0, so smp
+            // on escape (which terminates the path) and never Lambda0, so lam
             // is unchanged; the active-shape stack is written when it moved.
             L.thr[s] = make_float4(P.Throughput.x, P.Throughput.y, P.Throughput.z, P.Throughput.w);
             L.prob[s] = make_float4(P.Probability.x, P.Probability.y, P.Probability.z, P.Probability.w);
@@ -949,7 +973,7 @@ __global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MIN
             }
             *A = Val;
             completed = true;
-            GenerateNewPath(S, L, F, Pm, G, s, x, y, O, V);
+            GenerateNewPath(S, L, F, Pm, G, s, x, y, O, V, (act.x & act.y) == 0xFFFFFFFFu);
         }
     }
     // Completed paths per wave (ptGetStats): one counter word per 64 slots,
@@ -1112,6 +1136,16 @@ hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st)
     if (!L.order || L.tile_count == 0) return hipSuccess;
     hipLaunchKernelGGL(ptd::tile_order_kernel, dim3(1), dim3(1024), 0, st, L.tilecost, L.order, L.tile_base,
                        L.tile_count);
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_atlas_tile(const float4* src, float4* dst, uint32_t w, uint32_t h, uint32_t layers, hipStream_t st)
+{
+    uint64_t texels = (uint64_t)w * h * layers;
+    if (texels == 0) return hipSuccess;
+    uint64_t blocks = (texels + 255) / 256;
+    hipLaunchKernelGGL(ptd::atlas_tile_kernel, dim3((uint32_t)(blocks < 65536 ? blocks : 65536)), dim3(256), 0, st, src,
+                       dst, w, h, texels);
     return hipGetLastError();
 }
 

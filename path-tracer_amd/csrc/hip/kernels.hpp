@@ -27,7 +27,7 @@ struct dslots {
     float2* uv;         // compact hit: coords.y, coords.z
     float4* thr;        // throughput[4]
     float4* prob;       // probability[4]
-    float4* smp;        // sample.xyz, normalized lambda0
+    float* lam;         // normalized lambda0 (a live path's Sample is always 0: StorePathVertex)
     uint2* act;         // active-shape stack (2 x u16 pairs)
     uint16_t* pos;      // per slot: position of its current ray (high byte) and of
                         // its last traced hit (low byte) within its tile (TileOrder)
@@ -90,6 +90,9 @@ hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st);
 // (b % nranks != rank) before a frame-end reduce.
 hipError_t pt_launch_zero_unowned(float4* accum, uint32_t width, uint32_t height, uint32_t rank, uint32_t nranks,
                                   hipStream_t st);
+// Packed row-major atlas (w x h texels per layer) -> AtlasIndex block layout;
+// needs w % 4 == 0 and h % 2 == 0.
+hipError_t pt_launch_atlas_tile(const float4* src, float4* dst, uint32_t w, uint32_t h, uint32_t layers, hipStream_t st);
 hipError_t pt_launch_rcp_check(unsigned long long* mismatches, hipStream_t st);
 hipError_t pt_launch_xdiv_check(uint64_t n, uint32_t seed, unsigned long long* mismatches, hipStream_t st);
 hipError_t pt_launch_trace_rays(const ptd::dscene& S, uint32_t n, const float* origins, const uint32_t* vel,

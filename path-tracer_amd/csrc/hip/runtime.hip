@@ -100,6 +100,7 @@ struct pt_scene {
     dbuf<pt_packed_mesh_node> mesh_nodes;
     dbuf<pt_packed_camera> cameras;
     dbuf<float> atlas;
+    bool atlas_tiled = false;    // atlas in AtlasIndex 4x2-texel blocks
     uint32_t camera_count = 0;
     uint32_t stack_needed = 0;   // max traversal stack entries (TLAS + BLAS)
     uint32_t mats = PT_MATS_ALL; // material types referenced by shapes (shade specialisation)
@@ -135,7 +136,8 @@ struct pt_basic_renderer {
     uint32_t rank = 0, nranks = 1;
     uint32_t tiles_x = 0;
     ptd::dslots slots{};
-    dbuf<float4> ray, hit, thr, prob, smp;
+    dbuf<float4> ray, hit, thr, prob;
+    dbuf<float> lam;                    // lambda0 per slot (Sample is 0 between rounds)
     dbuf<float2> uv;
     dbuf<uint2> act;
     dbuf<uint16_t> pos;                 // TileOrder positions (kernels.hip)
@@ -520,7 +522,20 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     if (first || (dirty & PT_SCENE_DIRTY_TEXTURES)) {
         PT_HIP(s->textures.upload(p->textures, p->texture_count));
         size_t atlas_floats = (size_t)p->atlas_width * p->atlas_height * 4 * p->atlas_layer_count;
-        PT_HIP(s->atlas.upload(p->atlas, p->atlas ? atlas_floats : 0));
+        s->atlas_tiled = p->atlas && p->atlas_width % 4 == 0 && p->atlas_height % 2 == 0;
+        if (s->atlas_tiled) {
+            // Upload row-major, then re-lay the texels in 4x2 blocks
+            // (AtlasIndex, pt_device.hpp) on the device.
+            dbuf<float> stage;
+            struct release_stage { dbuf<float>& b; ~release_stage() { b.release(); } } guard{stage};
+            PT_HIP(stage.upload(p->atlas, atlas_floats));
+            PT_HIP(s->atlas.alloc(atlas_floats));
+            PT_HIP(pt_launch_atlas_tile(reinterpret_cast<const float4*>(stage.ptr), reinterpret_cast<float4*>(s->atlas.ptr),
+                                        p->atlas_width, p->atlas_height, p->atlas_layer_count, d->stream));
+            PT_HIP(hipStreamSynchronize(d->stream));
+        } else {
+            PT_HIP(s->atlas.upload(p->atlas, p->atlas ? atlas_floats : 0));
+        }
     }
     if (first || (dirty & PT_SCENE_DIRTY_MATERIALS)) PT_HIP(s->material.upload(p->material_data, p->material_word_count));
     if (first || (dirty & PT_SCENE_DIRTY_SHAPES)) {
@@ -558,6 +573,7 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     D.atlas_w = p->atlas_width;
     D.atlas_h = p->atlas_height;
     D.atlas_layers = p->atlas ? p->atlas_layer_count : 0;
+    D.atlas_tiled = s->atlas_tiled ? 1u : 0u;
     D.fast_div = FastDivBoxes(p) ? 1u : 0u;
     s->mats = SceneMaterialMask(p);
     uint32_t types = s->mats & (PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_TRANSLUCENT);
@@ -717,7 +733,7 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     if (n > 0xFFFFFFFFull / 2) { SetError("too many slots"); delete r; return nullptr; }
     uint32_t ns = (uint32_t)n;
     bool ok = r->ray.alloc(ns) == hipSuccess && r->hit.alloc(ns) == hipSuccess && r->thr.alloc(ns) == hipSuccess &&
-              r->prob.alloc(ns) == hipSuccess && r->smp.alloc(ns) == hipSuccess && r->uv.alloc(ns) == hipSuccess &&
+              r->prob.alloc(ns) == hipSuccess && r->lam.alloc(ns) == hipSuccess && r->uv.alloc(ns) == hipSuccess &&
               r->act.alloc(ns) == hipSuccess && r->pos.alloc(ns) == hipSuccess && r->slotof.alloc(ns) == hipSuccess &&
               r->outcome.alloc((size_t)(ns / 256) * 4 * ptd::PT_OUTCOME_CLASSES + 1) == hipSuccess &&
               r->tilecost.alloc((size_t)(ns / 256) * 4 + 1) == hipSuccess && r->order.alloc(ns / 256 + 1) == hipSuccess &&
@@ -725,7 +741,7 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     if (ok && ns) {
         ok = hipMemset(r->ray.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->hit.ptr, 0, (size_t)ns * 16) == hipSuccess &&
              hipMemset(r->thr.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->prob.ptr, 0, (size_t)ns * 16) == hipSuccess &&
-             hipMemset(r->smp.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->uv.ptr, 0, (size_t)ns * 8) == hipSuccess &&
+             hipMemset(r->lam.ptr, 0, (size_t)ns * 4) == hipSuccess && hipMemset(r->uv.ptr, 0, (size_t)ns * 8) == hipSuccess &&
              hipMemset(r->act.ptr, 0, (size_t)ns * 8) == hipSuccess && hipMemset(r->done.ptr, 0, (size_t)(ns / 64 + 1) * 4) == hipSuccess &&
              hipMemset(r->outcome.ptr, 0, ((size_t)(ns / 256) * 4 * ptd::PT_OUTCOME_CLASSES + 1) * 8) == hipSuccess;
         // Identity TileOrder until the first Reset sorts the rays.
@@ -741,7 +757,7 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     }
     if (!ok) {
         SetError("renderer slot allocation failed (%u slots)", ns);
-        r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->smp.release(); r->uv.release(); r->act.release();
+        r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->lam.release(); r->uv.release(); r->act.release();
         r->pos.release(); r->slotof.release(); r->outcome.release(); r->tilecost.release(); r->order.release();
         r->done.release();
         delete r;
@@ -752,7 +768,7 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     r->slots.uv = r->uv.ptr;
     r->slots.thr = r->thr.ptr;
     r->slots.prob = r->prob.ptr;
-    r->slots.smp = r->smp.ptr;
+    r->slots.lam = r->lam.ptr;
     r->slots.act = r->act.ptr;
     r->slots.pos = r->pos.ptr;
     r->slots.slotof = r->slotof.ptr;
@@ -790,7 +806,7 @@ void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
 {
     if (!r) return;
     if (d) { (void)hipSetDevice(d->id); (void)hipStreamSynchronize(d->stream); }
-    r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->smp.release();
+    r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->lam.release();
     r->uv.release(); r->act.release(); r->pos.release(); r->slotof.release(); r->outcome.release();
     r->tilecost.release(); r->order.release();
     r->done.release();
@@ -901,7 +917,8 @@ int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state*
     PT_HIP(hipSetDevice(d->id));
     PT_HIP(hipStreamSynchronize(d->stream));
     uint32_t n = r->slots.n;
-    std::vector<float4> ray(n), hit(n), thr(n), prob(n), smp(n);
+    std::vector<float4> ray(n), hit(n), thr(n), prob(n);
+    std::vector<float> lam(n);
     std::vector<float2> uv(n);
     std::vector<uint2> act(n);
     std::vector<uint16_t> pos(n);
@@ -923,7 +940,7 @@ int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state*
     PT_HIP(hipMemcpy(ray.data(), r->ray.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
     PT_HIP(hipMemcpy(thr.data(), r->thr.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
     PT_HIP(hipMemcpy(prob.data(), r->prob.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
-    PT_HIP(hipMemcpy(smp.data(), r->smp.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
+    PT_HIP(hipMemcpy(lam.data(), r->lam.ptr, (size_t)n * 4, hipMemcpyDeviceToHost));
     PT_HIP(hipMemcpy(act.data(), r->act.ptr, (size_t)n * 8, hipMemcpyDeviceToHost));
     PT_HIP(hipMemcpy(pos.data(), r->pos.ptr, (size_t)n * 2, hipMemcpyDeviceToHost));
     uint32_t W = r->buffer->width, H = r->buffer->height;
@@ -943,10 +960,10 @@ int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state*
         O.hit.packed_tangent = bits(hit[qh].w);
         O.hit.u = uv[qh].x;
         O.hit.v = uv[qh].y;
-        O.lambda0 = smp[s].w;
+        O.lambda0 = lam[s];
         O.throughput[0] = thr[s].x; O.throughput[1] = thr[s].y; O.throughput[2] = thr[s].z; O.throughput[3] = thr[s].w;
         O.probability[0] = prob[s].x; O.probability[1] = prob[s].y; O.probability[2] = prob[s].z; O.probability[3] = prob[s].w;
-        O.sample[0] = smp[s].x; O.sample[1] = smp[s].y; O.sample[2] = smp[s].z;
+        O.sample[0] = O.sample[1] = O.sample[2] = 0.0f;   // StorePathVertex (kernels.hip)
         O.active01 = act[s].x;
         O.active23 = act[s].y;
     }
