@@ -32,7 +32,7 @@ HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # records, independent of this build's layout): extend reads the 20-B ray and
 # writes the 24-B hit; shade reads path 60 + ray/hit 44 and writes ray 20 +
 # path vertex 52.  Sum = the 220 B/ray whole-path figure.
-ALG_BYTES = {"extend": 44, "shade": 176}
+ALG_BYTES = {"extend": 44, "shade": 176, "round": 220}   # round: fused extend + shade (small partitions)
 L2_PEAK_GBPS = 34500.0   # aggregate L2 bandwidth (MI355X_MICROARCH.md § L2)
 PATH_BYTES_PER_RAY = 220  # SURVEY.md §8(d) whole-path definition
 
@@ -202,6 +202,7 @@ def main():
     dt = time.perf_counter() - t0
     n_ext, ms_ext = dev.kernel_stats(1)
     n_sh, ms_sh = dev.kernel_stats(2)
+    n_rd, ms_rd = dev.kernel_stats(5)    # fused rounds (a partition that fits the GPU at once)
     dev.set_profiling(False)
 
     # Traversal counters of one extra extend over the current rays (outside
@@ -238,12 +239,12 @@ def main():
         return
 
     mrays = rays / dt / 1e6
-    avg_ext = ms_ext / max(n_ext, 1)
-    avg_sh = ms_sh / max(n_sh, 1)
-    kernels = {
-        "extend": {"avg_ms": avg_ext, "gbps": ALG_BYTES["extend"] * slots_owned / (avg_ext * 1e-3) / 1e9},
-        "shade": {"avg_ms": avg_sh, "gbps": ALG_BYTES["shade"] * slots_owned / (avg_sh * 1e-3) / 1e9},
-    }
+    avg_ext = ms_ext / max(n_ext, 1) if n_ext else ms_rd / max(n_rd, 1)   # traversal-level cache rate below
+    kernels = {}
+    for name, n_k, ms_k in (("extend", n_ext, ms_ext), ("shade", n_sh, ms_sh), ("round", n_rd, ms_rd)):
+        if n_k:
+            avg = ms_k / n_k
+            kernels[name] = {"avg_ms": avg, "gbps": ALG_BYTES[name] * slots_owned / (avg * 1e-3) / 1e9}
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
     achieved = kernels[dom]["gbps"]
     traffic, traffic_src = measured_traffic(dom)
@@ -284,8 +285,8 @@ def main():
             "traffic_source": traffic_src,
             "alg_bytes_per_launch": ALG_BYTES[dom] * slots_owned,
             "alg_bytes_per_slot": ALG_BYTES[dom],
-            "launch_avg_ms": {"extend": round(avg_ext, 4), "shade": round(avg_sh, 4)},
-            "launches_timed": {"extend": n_ext, "shade": n_sh, "every_nth_step": args.profile_period},
+            "launch_avg_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
+            "launches_timed": {"extend": n_ext, "shade": n_sh, "round": n_rd, "every_nth_step": args.profile_period},
             "path_gbps_220B_per_ray": round(PATH_BYTES_PER_RAY * rays / dt / 1e9, 2),
         },
         # What bounds the dominant kernel instead of HBM (PMC, same profile):

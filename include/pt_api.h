@@ -96,7 +96,8 @@ enum {
     PT_KERNEL_SHADE   = 2,
     PT_KERNEL_RESOLVE = 3,
     PT_KERNEL_PREVIEW = 4,
-    PT_KERNEL_COUNT   = 5,
+    PT_KERNEL_ROUND   = 5,   /* fused extend + shade of a small partition (one launch per round) */
+    PT_KERNEL_COUNT   = 6,
 };
 
 /* resolve_parameters (src/integrator/integrator.hpp:12-48). */
@@ -192,6 +193,12 @@ uint32_t           ptBasicRendererSlotCount(pt_basic_renderer* renderer);
  * renderer that fills the GPU; more for small partitions);
  * each kernel launch covers one group's tiles. */
 uint32_t           ptBasicRendererRunGroups(pt_basic_renderer* renderer);
+/* Fused rounds: 0 = never (extend then shade launches), 1 = automatic (one
+ * extend+shade launch per round when every tile of the renderer fits on the
+ * GPU at once: a rank's share of a strongly scaled frame), 2 = whenever the
+ * scene allows (no spilled traversal stack).  Results are identical in every
+ * mode.  Default 1, or the PT_ROUND_FUSED environment variable. */
+int                ptSetBasicRendererFusedRounds(pt_basic_renderer* renderer, int mode);
 /* Work done since the last Reset: rays traced (one per owned pixel per round)
  * and paths completed (accumulator sample increments, basic_scatter.glsl:
  * 350-359).  Either pointer may be NULL.  Synchronises the device stream. */

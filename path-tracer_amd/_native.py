@@ -143,6 +143,7 @@ TONE_MAPPING_CLAMP, TONE_MAPPING_REINHARD, TONE_MAPPING_HABLE, TONE_MAPPING_ACES
  PREVIEW_RENDER_MODE_MATERIAL_INDEX, PREVIEW_RENDER_MODE_PRIMITIVE_INDEX, PREVIEW_RENDER_MODE_MESH_COMPLEXITY,
  PREVIEW_RENDER_MODE_SCENE_COMPLEXITY) = range(7)
 KERNEL_PREVIEW = 4
+KERNEL_ROUND = 5     # fused extend + shade (partitions that fit the GPU at once)
 
 _vp = C.c_void_p
 _u32 = C.c_uint32
@@ -231,6 +232,7 @@ HIP_API = {
     "ptRunBasicRenderer": (_i32, [_vp, _vp, _u32]),
     "ptBasicRendererSlotCount": (_u32, [_vp]),
     "ptBasicRendererRunGroups": (_u32, [_vp]),
+    "ptSetBasicRendererFusedRounds": (_i32, [_vp, _i32]),
     "ptGetStats": (_i32, [_vp, _vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "ptReadBasicRendererState": (_i32, [_vp, _vp, _vp]),
     "ptTraceRays": (_i32, [_vp, _vp, _u32, _fptr, _u32ptr, _fptr, _vp]),

@@ -610,6 +610,10 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
 
 // --- kernels -------------------------------------------------------------------
 
+#ifndef PT_WAVE_PRIO
+#define PT_WAVE_PRIO 0
+#endif
+
 // One block per tile (the slot count is a multiple of 256): TileOrder needs
 // every thread of the block, so no thread returns early.
 #ifndef PT_SHADE_ORDER
@@ -714,8 +718,24 @@ PT_DEV void ExtendRay(const dscene& S, const Src& src, tstack<SPILL, CAP, E>& st
         lane_state Ln;
         LaneBegin(S, Ln, O, V, D);
         no_stats ns;
-        if (S.g.ShapeCount != 0)
+        if (S.g.ShapeCount != 0) {
+#if PT_WAVE_PRIO
+            // A wave still traversing after 32 / 64 / 96 steps raises its
+            // issue priority: the SIMD's arbiter then serves the long waves
+            // that set the launch's end before the short ones beside them.
+            uint32_t it = 0;
+            while (!LaneStep<SPILL, CAP, Src, no_stats, true, E>(S, Ln, st, src, slot, ns)) {
+                if ((++it & 31u) == 0) {
+                    uint32_t u = __builtin_amdgcn_readfirstlane(it);
+                    if (u == 32) __builtin_amdgcn_s_setprio(1);
+                    else if (u == 64) __builtin_amdgcn_s_setprio(2);
+                    else if (u == 96) __builtin_amdgcn_s_setprio(3);
+                }
+            }
+#else
             while (!LaneStep<SPILL, CAP, Src, no_stats, true, E>(S, Ln, st, src, slot, ns)) {}
+#endif
+        }
         src.store(slot, Ln);
         if (Ln.Shape == SHAPE_INDEX_NONE) {
             cls = 4;
@@ -729,6 +749,25 @@ PT_DEV void ExtendRay(const dscene& S, const Src& src, tstack<SPILL, CAP, E>& st
     src.outcome(slot, cls, S.mat_classes != 0);
 }
 
+// One tile of extend: thread i traces the ray at position tile*256 + i.
+template <class Src, bool SPILL, int CAP, class E>
+PT_DEV void ExtendTile(const dscene& S, const Src& src, uint32_t n, uint32_t* spill, uint32_t spill_stride, E* smem,
+                       uint32_t tile, bool timed)
+{
+    uint64_t t0 = timed ? __builtin_amdgcn_s_memtime() : 0;
+    uint32_t slot = tile * 256 + threadIdx.x;
+    if (slot >= n) return;
+    tstack<SPILL, CAP, E> st;
+    st.lds = &smem[threadIdx.x];
+    st.spill = spill + slot;
+    st.stride = spill_stride;
+    ExtendRay<SPILL, CAP, E>(S, src, st, slot);
+    if constexpr (std::is_same<Src, ray_source_slots>::value) {
+        if (timed && (threadIdx.x & 63u) == 0)
+            src.L.tilecost[tile * 4 + (threadIdx.x >> 6)] = (uint32_t)(__builtin_amdgcn_s_memtime() - t0);
+    }
+}
+
 template <class Src, bool SPILL, int MINW, int CAP, class E = uint32_t>
 __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, uint32_t n, uint32_t* spill,
                                                                   uint32_t spill_stride)
@@ -738,25 +777,15 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
     // longest in the previous round first (tile_order_kernel), so the
     // kernel's tail holds short blocks; each wave records its own time.
     uint32_t tile = blockIdx.x;
-    uint64_t t0 = 0;
+    bool timed = false;
     if constexpr (std::is_same<Src, ray_source_slots>::value) {
         tile += src.L.tile_base;
         if (src.L.order) {
             tile = src.L.order[blockIdx.x];
-            t0 = __builtin_amdgcn_s_memtime();
+            timed = true;
         }
     }
-    uint32_t slot = tile * 256 + threadIdx.x;
-    if (slot >= n) return;
-    tstack<SPILL, CAP, E> st;
-    st.lds = &smem[threadIdx.x];
-    st.spill = spill + slot;
-    st.stride = spill_stride;
-    ExtendRay<SPILL, CAP, E>(S, src, st, slot);
-    if constexpr (std::is_same<Src, ray_source_slots>::value) {
-        if (src.L.order && (threadIdx.x & 63u) == 0)
-            src.L.tilecost[tile * 4 + (threadIdx.x >> 6)] = (uint32_t)(__builtin_amdgcn_s_memtime() - t0);
-    }
+    ExtendTile<Src, SPILL, CAP, E>(S, src, n, spill, spill_stride, smem, tile, timed);
 }
 
 // Longest-first dispatch order for the next extend: tiles by their slowest
@@ -890,17 +919,14 @@ __global__ __launch_bounds__(256) void finalize_kernel(dscene S, uint32_t n, con
 #ifndef PT_SHADE_DIFFUSE_MINW
 #define PT_SHADE_DIFFUSE_MINW 5
 #endif
+// One tile of shade (basic_scatter.glsl:main for the tile's 256 slots).
 template <uint32_t MATS>
-__global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MINW : 1) void shade_kernel(dscene S, dslots L, dframe F,
-                                                                                    dparams Pm)
+PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const dparams& Pm, uint32_t tile)
 {
     // One block per tile, no early exit (TileOrder).  ShadeOrder: thread u
     // shades the slot whose ray sits at ShadePosition(u), so the waves of a
     // tile run the surface path or the escape path, mostly not both; path
     // state is read and written by slot (gathers within the tile's records).
-    // Tiles in extend's longest-first order too: tiles with long traversals
-    // also shade more hits (C5 shade -3 %).
-    const uint32_t tile = L.order ? L.order[blockIdx.x] : L.tile_base + blockIdx.x;
     const uint32_t base = tile * 256;
 #if PT_SHADE_ORDER
     const uint64_t* om = L.outcome + (size_t)tile * (4 * PT_OUTCOME_CLASSES);
@@ -981,6 +1007,35 @@ __global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MIN
     uint64_t cm = __ballot(completed);
     if ((threadIdx.x & 63u) == 0) L.done[(base | threadIdx.x) >> 6] += (uint32_t)__popcll(cm);
     TileOrderStoreRay(L, s, valid, O, V, p16 >> 8);
+}
+
+template <uint32_t MATS>
+__global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MINW : 1) void shade_kernel(dscene S, dslots L, dframe F,
+                                                                                    dparams Pm)
+{
+    // Tiles in extend's longest-first order too: tiles with long traversals
+    // also shade more hits (C5 shade -3 %).
+    ShadeTile<MATS>(S, L, F, Pm, L.order ? L.order[blockIdx.x] : L.tile_base + blockIdx.x);
+}
+
+// One round (extend + shade) of a tile per block, for partitions whose tiles
+// all fit on the GPU at once (a rank's share of a strongly scaled frame):
+// a tile is shaded as soon as its own rays are traced, so the shading of
+// most tiles runs beside the few long traversals that end the round instead
+// of after them, and one launch replaces two.  Same per-tile work and order
+// as extend_kernel then shade_kernel, so the results are identical.
+template <uint32_t MATS, int CAP, class E>
+__global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MINW : 1) void round_kernel(
+    dscene S, dslots L, dframe F, dparams Pm)
+{
+    __shared__ E smem[CAP * 256];
+    const uint32_t tile = L.order ? L.order[blockIdx.x] : L.tile_base + blockIdx.x;
+    ExtendTile<ray_source_slots, false, CAP, E>(S, ray_source_slots{L, F}, L.n, nullptr, 0, smem, tile,
+                                                 L.order != nullptr);
+    // The tile's hits and outcome masks (global, written by all four waves)
+    // are complete and visible to the block after the barrier.
+    __syncthreads();
+    ShadeTile<MATS>(S, L, F, Pm, tile);
 }
 
 // Exhaustive check of FastRcp: every bit pattern d = i (i < 2^32); counts
@@ -1162,6 +1217,46 @@ hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const pt
                             hipStream_t st)
 {
     return LaunchExtend(S, ptd::ray_source_slots{L, F}, L.n, L.tile_count, spill, st);
+}
+
+// Fused rounds (round_kernel): the default extend variant's LDS stack
+// without spill, one instantiation per shade material mask and stack entry
+// width.  Capacity = the tiles the GPU holds at once (blocks per CU at the
+// kernel's occupancy x CUs); a larger partition runs extend + shade.
+template <uint32_t MATS, class E>
+static const void* RoundKernel() { return reinterpret_cast<const void*>(&ptd::round_kernel<MATS, 20, E>); }
+
+static const void* RoundKernelFor(uint32_t mats, bool stack16)
+{
+    switch (pt_shade_mats(mats)) {
+    case PT_MATS_DIFFUSE: return stack16 ? RoundKernel<PT_MATS_DIFFUSE, uint16_t>() : RoundKernel<PT_MATS_DIFFUSE, uint32_t>();
+    case PT_MATS_DIFFUSE | PT_MATS_METAL:
+        return stack16 ? RoundKernel<PT_MATS_DIFFUSE | PT_MATS_METAL, uint16_t>()
+                       : RoundKernel<PT_MATS_DIFFUSE | PT_MATS_METAL, uint32_t>();
+    default: return stack16 ? RoundKernel<PT_MATS_ALL, uint16_t>() : RoundKernel<PT_MATS_ALL, uint32_t>();
+    }
+}
+
+uint32_t pt_round_capacity(uint32_t scene_mats, bool stack16, uint32_t cu_count)
+{
+    if (pt_extend_variant() != 0) return 0;   // round_kernel has the default variant's 20-entry stack
+    static int per_cu[3][2] = {{-1, -1}, {-1, -1}, {-1, -1}};   // by shade mask, stack entry width
+    uint32_t m = pt_shade_mats(scene_mats);
+    int& c = per_cu[m == PT_MATS_DIFFUSE ? 0 : m == (PT_MATS_DIFFUSE | PT_MATS_METAL) ? 1 : 2][stack16 ? 1 : 0];
+    if (c < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&c, RoundKernelFor(scene_mats, stack16), 256, 0) != hipSuccess)
+        c = 0;
+    return (uint32_t)c * cu_count;
+}
+
+hipError_t pt_launch_round(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
+                           uint32_t scene_mats, hipStream_t st)
+{
+    if (L.n == 0 || L.tile_count == 0) return hipSuccess;
+    if (L.spill || pt_extend_variant() != 0) return hipErrorNotSupported;
+    const void* k = RoundKernelFor(scene_mats, S.stack16 != 0);
+    void* args[] = {const_cast<ptd::dscene*>(&S), const_cast<ptd::dslots*>(&L), const_cast<ptd::dframe*>(&F),
+                    const_cast<ptd::dparams*>(&P)};
+    return hipLaunchKernel(k, dim3(L.tile_count), dim3(256), args, 0, st);
 }
 
 // Shade instantiations by material-type mask: the smallest superset of the

@@ -86,6 +86,12 @@ hipError_t pt_launch_resolve(const float4* accum, uint32_t n, float brightness, 
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
                            uint32_t scene_mats, hipStream_t st);
 hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st);
+// Fused round (extend + shade per tile in one launch, round_kernel): the
+// tiles the GPU can hold at once for this scene (0: not available), and the
+// launch (hipErrorNotSupported when the scene needs a spilled stack).
+uint32_t pt_round_capacity(uint32_t scene_mats, bool stack16, uint32_t cu_count);
+hipError_t pt_launch_round(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
+                           uint32_t scene_mats, hipStream_t st);
 // Zeroes the rows of a sample buffer outside a renderer's 16-row bands
 // (b % nranks != rank) before a frame-end reduce.
 hipError_t pt_launch_zero_unowned(float4* accum, uint32_t width, uint32_t height, uint32_t rank, uint32_t nranks,

@@ -128,6 +128,14 @@ struct pt_preview {
     bool rendered = false;
 };
 
+namespace {
+int FusedDefault()
+{
+    const char* e = getenv("PT_ROUND_FUSED");
+    return e ? atoi(e) : 1;
+}
+}  // namespace
+
 struct pt_basic_renderer {
     pt_basic_renderer_params params{};
     pt_device* dev = nullptr;
@@ -152,6 +160,7 @@ struct pt_basic_renderer {
     // tiles (a partition too small to fill the GPU: strong scaling).
     static constexpr uint32_t MAX_GROUPS = 4;
     uint32_t groups = 1;
+    int fused = FusedDefault();         // fused rounds mode (ptSetBasicRendererFusedRounds)
     hipStream_t gstream[MAX_GROUPS] = {};
     hipEvent_t gevent[MAX_GROUPS] = {};
     hipEvent_t fork = nullptr;
@@ -838,6 +847,19 @@ int ptResetBasicRenderer(pt_device* d, pt_basic_renderer* r)
 }
 
 // RunBasicRenderer (basic.cpp:306-332)
+// Fused rounds (round_kernel) when every tile of the launch fits on the GPU
+// at once -- a rank's share of a strongly scaled frame -- and the scene needs
+// no spilled stack (renderer mode 1); mode 0 never fuses, mode 2 fuses
+// whenever the kernel applies (tests and A/B).
+static bool RoundFused(const pt_basic_renderer* r, const ptd::dslots& g)
+{
+    const int mode = r->fused;
+    if (mode == 0 || g.spill || g.tile_count == 0) return false;
+    uint32_t cap = pt_round_capacity(r->scene->mats, r->scene->d.stack16 != 0, r->dev->cu_count);
+    if (cap == 0) return false;
+    return mode == 2 || g.tile_count <= cap;
+}
+
 int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
 {
     if (!d) { SetError("null device"); return -1; }
@@ -871,6 +893,13 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
         bool sort = r->slots.order && (r->order_tick++ % TileOrderPeriod()) == 0;
         for (uint32_t g = 0; g < G; g++) {
             event_pair ep{};
+            if (RoundFused(r, gs[g])) {
+                if (int e = BeginTimed(d, PT_KERNEL_ROUND, ep, sampled, st[g])) return e;
+                PT_HIP(pt_launch_round(r->scene->d, gs[g], F, P, r->scene->mats, st[g]));
+                if (int e = EndTimed(d, ep)) return e;
+                if (sort) PT_HIP(pt_launch_tile_order(gs[g], st[g]));
+                continue;
+            }
             if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled, st[g])) return e;
             PT_HIP(pt_launch_extend(r->scene->d, gs[g], F, r->slots.spill, st[g]));
             if (int e = EndTimed(d, ep)) return e;
@@ -890,6 +919,13 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
 }
 
 uint32_t ptBasicRendererRunGroups(pt_basic_renderer* r) { return r ? r->groups : 0; }
+
+int ptSetBasicRendererFusedRounds(pt_basic_renderer* r, int mode)
+{
+    if (!r || mode < 0 || mode > 2) { SetError("ptSetBasicRendererFusedRounds: bad argument"); return -1; }
+    r->fused = mode;
+    return 0;
+}
 
 // Counters of the work done since the last Reset: rays traced (every owned
 // pixel's slot traces one ray per round, K3) and paths completed (the

@@ -224,6 +224,10 @@ class BasicRenderer:
         """Tile groups advanced on separate streams (ptBasicRendererRunGroups)."""
         return int(N.hip_lib().ptBasicRendererRunGroups(self._h))
 
+    def set_fused_rounds(self, mode: int):
+        """0 never / 1 automatic / 2 whenever possible (ptSetBasicRendererFusedRounds)."""
+        _check(N.hip_lib().ptSetBasicRendererFusedRounds(self._h, int(mode)), "ptSetBasicRendererFusedRounds")
+
     def reset(self):
         _check(N.hip_lib().ptResetBasicRenderer(self.device.handle, self._h), "ptResetBasicRenderer")
 

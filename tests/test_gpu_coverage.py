@@ -15,6 +15,9 @@ against the CPU oracle bit for bit):
   (application.cpp:52-66,88-115);
 * ptGetStats and the RCCL frame-end reduce (idempotent over progressive
   frames);
+* fused rounds (one extend+shade launch per round, round_kernel) against
+  the separate launches and the oracle, including a full C3 frame forced
+  through the fused kernel;
 * two processes rendering their bands with the product renderer and summing
   over gloo (the CPU stand-in for the RCCL reduce; RCCL refuses two ranks on
   one device), equal to the single-process frame.
@@ -204,6 +207,38 @@ def test_comm_reduce_is_idempotent_over_progressive_frames(pt, dev):
             x.run(1)
     comm.close()
     o.close()
+    for x in (r, sb, ds):
+        x.close()
+    s.close()
+
+
+# (config, W, H, schedule): small frames (automatic mode fuses them), a C5
+# mixed-material frame with a medium, and the full C3 frame (8160 tiles, more
+# than the GPU holds at once: forced with mode 2).
+FUSED_CASES = [(3, 160, 96, [2, 1, 3]), (5, 128, 64, [2, 1, 2]), (2, 96, 96, [2, 1, 2]), (3, 1920, 1080, [2, 1])]
+
+
+@pytest.mark.parametrize("config,W,H,schedule", FUSED_CASES)
+def test_fused_rounds_bit_exact(pt, dev, config, W, H, schedule):
+    """round_kernel (extend + shade of a tile in one block) gives the same
+    state and image as extend_kernel then shade_kernel, and as the oracle."""
+    out = {m: render_pair(pt, dev, config, W, H, schedule, fused=m) for m in (0, 2)}
+    for m in (0, 2):
+        gs, os_, ga, oa = out[m]
+        compare_state(gs, os_)
+        assert np.array_equal(bits(ga), bits(oa)), f"fused mode {m}"
+    assert oa[..., 3].sum() > 0
+
+
+def test_fused_rounds_mode_argument(pt, dev):
+    s = pt.Scene.config(1)
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    sb = pt.SampleBuffer(dev, 32, 32)
+    r = pt.BasicRenderer(dev, ds, sb)
+    with pytest.raises(pt.PathTracerError):
+        r.set_fused_rounds(3)
+    r.set_fused_rounds(1)
     for x in (r, sb, ds):
         x.close()
     s.close()

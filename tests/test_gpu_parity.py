@@ -138,15 +138,18 @@ def test_deep_stack_spills_bit_exact(pt, dev, tmp_path):
 
 
 def render_pair(pt, dev, config, W, H, schedule, camera=0, flags=3, termination=0.0, rank=0, nranks=1,
-                scene=None):
+                scene=None, fused=None):
     """The same Reset + Run(schedule...) on the HIP renderer and the oracle:
-    (GPU state, oracle state, GPU accumulator, oracle accumulator)."""
+    (GPU state, oracle state, GPU accumulator, oracle accumulator).
+    fused: the renderer's fused-rounds mode (None: its default)."""
     s = scene if scene is not None else scene_for(pt, config)
     ds = pt.DeviceScene(dev)
     ds.update(s)
     sb = pt.SampleBuffer(dev, W, H)
     r = pt.BasicRenderer(dev, ds, sb, rank=rank, nranks=nranks)
     o = oracle_lib.OracleRenderer(s.packs(), W, H, rank=rank, nranks=nranks)
+    if fused is not None:
+        r.set_fused_rounds(fused)
     for x in (r, o):
         x.RenderFlags = flags
         x.PathTerminationProbability = termination
@@ -260,12 +263,21 @@ def test_profiling_counts_kernels(pt, dev):
     dev.reset_kernel_stats()
     r.RenderFlags = 3
     r.reset()
+    r.set_fused_rounds(0)
     r.run(3)
     n_ext, ms_ext = dev.kernel_stats(1)
     n_sh, ms_sh = dev.kernel_stats(2)
-    dev.set_profiling(False)
-    # one extend + one shade per round and tile range (PT_RUN_PARTS)
+    # one extend + one shade per round and tile range (run groups)
     assert n_ext == n_sh and n_ext % 3 == 0 and n_ext >= 3 and ms_ext > 0 and ms_sh > 0
+    # a 64x64 frame fits the GPU at once: the automatic mode fuses its rounds
+    # into one launch each (kernel 5)
+    dev.reset_kernel_stats()
+    r.set_fused_rounds(1)
+    r.run(2)
+    n_rd, ms_rd = dev.kernel_stats(5)
+    assert dev.kernel_stats(1)[0] == 0 and dev.kernel_stats(2)[0] == 0
+    assert n_rd >= 2 and n_rd % 2 == 0 and ms_rd > 0
+    dev.set_profiling(False)
     r.close(); sb.close(); ds.close()
 
 

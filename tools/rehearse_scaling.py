@@ -72,6 +72,7 @@ def main():
             rays1, _ = r.stats()
             ne, me = dev.kernel_stats(1)
             ns_, ms = dev.kernel_stats(2)
+            nr, mr = dev.kernel_stats(5)
             dev.set_profiling(False)
             owned = int(np.sum(pt.owned_pixels(W, H, 0, n)))
             step_ms = dt / args.steps * 1e3
@@ -81,6 +82,7 @@ def main():
                 "rank0_ms_per_step": round(step_ms, 4),
                 "rank0_mrays_per_s": round((rays1 - rays0) / dt / 1e6, 1),
                 "extend_ms": round(me / max(ne, 1), 4), "shade_ms": round(ms / max(ns_, 1), 4),
+                "round_ms": round(mr / max(nr, 1), 4),
                 "predicted_frame_mrays_per_s": round(W * H / (step_ms * 1e-3) / 1e6, 1),
             }
             rows.append(row)
