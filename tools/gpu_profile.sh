@@ -10,7 +10,8 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/prof_$TAG
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
-B="$R/bench.py --steps 16 --warmup 2 --no-cpu-baseline"
+# the driver's exact bench command (BENCH_rNN.json "cmd")
+B="$R/bench.py --gpus 1 --steps 20 --warmup 5"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$O/trace" -o run -- python3 $B > "$O/trace.log" 2>&1
 rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 i=0
@@ -22,6 +23,7 @@ done
 python3 $R/profiles/pmc_summary.py "$O/pmc_summary.json" $(find "$O" -name "*counter_collection.csv") > "$O/pmc_summary.txt"
 cp $(find "$O/trace" -name "*kernel_stats.csv") "$O/kernel_stats.csv"
 cd "$R"
-timeout -k 10 400 python3 bench.py > "$O/bench.json.log" 2>&1; rc=$?; echo "bench rc=$rc"
+timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench.json.log" 2>&1; rc=$?; echo "bench rc=$rc"
 tail -1 "$O/bench.json.log" > "$O/bench.json"
 cat "$O/pmc_summary.txt"; cat "$O/bench.json"
+python3 $R/profiles/timed_region.py $(find "$O/trace" -name "*kernel_trace.csv") 20 "$O/timed_region.json"

@@ -9,8 +9,8 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 run = Path(sys.argv[1])
 s = json.loads((ROOT / run / "pmc_summary.json").read_text())
-out = {"profile": str(run), "command": "tools/gpu_profile.sh (bench.py C3 1920x1080, N=1)", "kernels": {}, "issue": {}}
-for k in ("extend", "raygen", "shade"):
+out = {"profile": str(run), "command": "tools/gpu_profile.sh (bench.py --gpus 1 --steps 20 --warmup 5: C3 1920x1080, N=1)", "kernels": {}, "issue": {}}
+for k in ("extend", "raygen", "shade", "round"):
     if k not in s:
         continue
     out["kernels"][k] = {x: int(s[k][x]) for x in ("hbm_bytes", "hbm_read_bytes", "hbm_write_bytes") if x in s[k]}
