@@ -70,7 +70,6 @@ PT_DEV void SetLevelRay(const dscene& S, lane_state& L, pt3 O, pt3 V)
 
 PT_DEV void LaneBegin(const dscene& S, lane_state& L, pt3 O, pt3 V, float Duration)
 {
-    SetLevelRay(S, L, O, V);
     L.Time = Duration;
     L.Shape = SHAPE_INDEX_NONE;
     L.Prim = 0;
@@ -80,6 +79,17 @@ PT_DEV void LaneBegin(const dscene& S, lane_state& L, pt3 O, pt3 V, float Durati
     L.blas = SHAPE_INDEX_NONE;
     L.na = __float_as_uint(S.shape_nodes[0].w);
     L.nb = __float_as_uint(S.shape_nodes[1].w);
+    if (L.na != 0) {
+        SetLevelRay(S, L, O, V);
+    } else {
+        // The TLAS root is a shape leaf (a one-shape scene): the first step
+        // transforms the ray into the shape's space and sets that level's
+        // reciprocal; the world-space one would never be read.
+        L.O = O;
+        L.V = V;
+        L.exact = false;
+        asm("" : "=v"(L.Y.x), "=v"(L.Y.y), "=v"(L.Y.z));
+    }
 }
 
 // IntersectShape for the analytic shapes (scene.glsl.inc:413-465).
@@ -428,9 +438,14 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP, SE>& st,
         L.Prim = fmiss ? L.Prim : L.na;
         L.C = v3(fmiss ? L.C.x : 1 - fU - fW, fmiss ? L.C.y : fU, fmiss ? L.C.z : fW);
         // Internal node: the reference's three-way decision (scene.glsl.inc:366-392).
+        // (The child set aside is pushed iff its own time is finite: one
+        // select of the time, not of two flags; `moved` as mask logic, not a
+        // select between the halves' flags, which the compiler lowered to
+        // exec-mask branches.)
         bool goB = TA > TB;
-        bool push = !face & (goB ? (TA < PT_INFINITY) : (TB < PT_INFINITY));
-        bool moved = face ? (L.na + 1 < L.nb) : (goB | (TA < PT_INFINITY));
+        float Tfar = goB ? TA : TB;
+        bool push = !face & (Tfar < PT_INFINITY);
+        bool moved = (face & (L.na + 1 < L.nb)) | (!face & (goB | (TA < PT_INFINITY)));
         if (push & (L.dB < 32)) {
             st.put(L.dT + L.dB++, BlasPush<SE>(S, goB ? aw0 : bw0, goB ? aw1 : bw1, L.na + (goB ? 0u : 1u)));
         }
