@@ -129,6 +129,11 @@ void      ptsMeshFaces(pts_mesh* mesh, uint32_t* indices);
  * OBJ + MTL), CreateEntity(Scene, Prefab, Parent) (scene.cpp:251-254). */
 void        ptsDefaultLoadModelOptions(pts_load_model_options* options);
 pts_texture* ptsLoadTexture(pts_scene* scene, const char* path, int type, const char* name);
+/* The 8-bit RGBA samples LoadTexture linearises (JPEG / PNG / BMP / TGA;
+ * stb_image's stbi_load(..., 4) semantics), for tests: returns 0 and the size
+ * in *width, *height; `rgba` (may be NULL for a size query) receives
+ * width*height*4 bytes. */
+int ptsLoadImageRGBA8(const char* path, uint32_t* width, uint32_t* height, uint8_t* rgba);
 pts_prefab* ptsLoadModelAsPrefab(pts_scene* scene, const char* path, const pts_load_model_options* options);
 pts_entity* ptsInstantiatePrefab(pts_scene* scene, pts_prefab* prefab, pts_entity* parent);
 uint32_t    ptsPrefabMeshCount(pts_prefab* prefab);

@@ -5,7 +5,7 @@ Import as `path_tracer_amd` via the loader in tests/conftest.py or bench.py
 (the directory name contains a hyphen).
 """
 from . import _native
-from .scene import (Scene, spectrum_coefficients, build_spectrum_table, load_spectrum_table, mesh_depth,
+from .scene import (Scene, load_image_rgba8, spectrum_coefficients, build_spectrum_table, load_spectrum_table, mesh_depth,
                     mesh_node_count, ENTITY_CONTAINER, ENTITY_CAMERA, ENTITY_MESH_INSTANCE, ENTITY_PLANE,
                     ENTITY_SPHERE, ENTITY_CUBE, MATERIAL_BASIC_DIFFUSE, MATERIAL_BASIC_METAL,
                     MATERIAL_BASIC_TRANSLUCENT, MATERIAL_OPENPBR, TEXTURE_RAW, TEXTURE_REFLECTANCE_WITH_ALPHA,

@@ -184,6 +184,7 @@ SCENE_API = {
     "ptsMeshFaces": (None, [_vp, _u32ptr]),
     "ptsDefaultLoadModelOptions": (None, [C.POINTER(pts_load_model_options)]),
     "ptsLoadTexture": (_vp, [_vp, C.c_char_p, _i32, C.c_char_p]),
+    "ptsLoadImageRGBA8": (_i32, [C.c_char_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), _vp]),
     "ptsLoadModelAsPrefab": (_vp, [_vp, C.c_char_p, C.POINTER(pts_load_model_options)]),
     "ptsInstantiatePrefab": (_vp, [_vp, _vp, _vp]),
     "ptsLoadScene": (_vp, [C.c_char_p]),

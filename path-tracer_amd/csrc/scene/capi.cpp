@@ -2,6 +2,7 @@
 // restatement.  Handles are the C++ objects themselves.
 #include "scene.hpp"
 #include "configs.hpp"
+#include "image.hpp"
 #include "../../../include/pt_scene.h"
 
 #include <cstring>
@@ -192,6 +193,18 @@ void ptsDefaultLoadModelOptions(pts_load_model_options* o)
     std::memset(o, 0, sizeof(*o));
     for (int i = 0; i < 4; i++) { o->vertex_transform[5 * i] = 1; o->normal_transform[5 * i] = 1; }
     for (int i = 0; i < 3; i++) o->texcoord_transform[4 * i] = 1;
+}
+
+int ptsLoadImageRGBA8(const char* path, uint32_t* w, uint32_t* h, uint8_t* rgba)
+{
+    int W = 0, H = 0;
+    std::vector<uint8_t> px;
+    std::string err;
+    if (!path || !LoadImageRGBA8(path, W, H, px, err)) { g_err = err.empty() ? "bad path" : err; return -1; }
+    if (w) *w = (uint32_t)W;
+    if (h) *h = (uint32_t)H;
+    if (rgba) std::memcpy(rgba, px.data(), px.size());
+    return 0;
 }
 
 pts_texture* ptsLoadTexture(pts_scene* s, const char* path, int type, const char* name)

@@ -5,7 +5,7 @@
 // linearised by pow(v / 255, 2.2) and alpha as v / 255; Radiance .hdr files
 // decode RGBE to linear floats with alpha 1.  This decoder follows the PNG
 // (ISO/IEC 15948) and Radiance RGBE specifications and applies those
-// conversions; it reads PNG of every colour type / bit depth (incl. palette,
+// conversions; it reads JPEG (jpeg.cpp), PNG of every colour type / bit depth (incl. palette,
 // tRNS and Adam7 interlacing), BMP, TGA and RLE or flat RGBE .hdr.
 #include "image.hpp"
 
@@ -472,14 +472,18 @@ bool DecodeBMP(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_
     return true;
 }
 
-// PNG, BMP or TGA (the format without a signature, tried last as stb does).
+// JPEG, PNG, BMP or TGA (the format without a signature, tried last as stb
+// does; stbi__load_main tries JPEG first: an SOI marker, after any 0xFF fill).
 bool DecodeLDR(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_t>& rgba8, std::string& err)
 {
     static const uint8_t png_sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+    size_t k = 0;
+    while (k < f.size() && f[k] == 0xFF) k++;
+    if (k >= 1 && k < f.size() && f[k] == 0xD8) return DecodeJPEG(f, W, H, rgba8, err);
     if (f.size() >= 8 && std::memcmp(f.data(), png_sig, 8) == 0) return DecodePNG(f, W, H, rgba8, err);
     if (f.size() >= 2 && f[0] == 'B' && f[1] == 'M') return DecodeBMP(f, W, H, rgba8, err);
     if (DecodeTGA(f, W, H, rgba8, err)) return true;
-    err = "unsupported image format (PNG, BMP, TGA, Radiance HDR)";
+    err = "unsupported image format (JPEG, PNG, BMP, TGA, Radiance HDR)";
     return false;
 }
 

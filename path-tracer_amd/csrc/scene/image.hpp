@@ -1,4 +1,4 @@
-// image.hpp — texture file decoding (PNG, BMP, TGA, Radiance HDR) for LoadTexture.
+// image.hpp — texture file decoding (JPEG, PNG, BMP, TGA, Radiance HDR) for LoadTexture.
 #pragma once
 
 #include <cstdint>
@@ -13,7 +13,10 @@ namespace pth {
 // linearised by pow(v / 255, 2.2), alpha v / 255; HDR decoded linearly.
 bool LoadImageFloat(const char* Path, int& Width, int& Height, std::vector<vec4>& Pixels, std::string& Error);
 
-// The 8-bit RGBA samples of a PNG / BMP / TGA (before linearisation), for tests.
+// The 8-bit RGBA samples of a JPEG / PNG / BMP / TGA (before linearisation), for tests.
 bool LoadImageRGBA8(const char* Path, int& Width, int& Height, std::vector<uint8_t>& RGBA, std::string& Error);
+
+// Baseline / progressive JPEG to RGBA8 with stb_image's output semantics (jpeg.cpp).
+bool DecodeJPEG(const std::vector<uint8_t>& File, int& Width, int& Height, std::vector<uint8_t>& RGBA, std::string& Error);
 
 }  // namespace pth

@@ -275,6 +275,17 @@ def mesh_node_count(mesh) -> int:
     return int(N.scene_lib().ptsMeshNodeCount(mesh))
 
 
+def load_image_rgba8(path) -> np.ndarray:
+    """The 8-bit RGBA samples LoadTexture linearises (ptsLoadImageRGBA8), H x W x 4."""
+    L = N.scene_lib()
+    w, h = C.c_uint32(0), C.c_uint32(0)
+    if L.ptsLoadImageRGBA8(str(path).encode(), C.byref(w), C.byref(h), None) != 0:
+        raise ValueError(L.ptsGetLastError().decode())
+    out = np.zeros((h.value, w.value, 4), dtype=np.uint8)
+    L.ptsLoadImageRGBA8(str(path).encode(), None, None, out.ctypes.data)
+    return out
+
+
 def spectrum_coefficients(rgb) -> np.ndarray:
     """GetParametricSpectrumCoefficients (spectrum.cpp:439-479)."""
     c = np.asarray(rgb, dtype=np.float32)
