@@ -12,6 +12,14 @@ namespace ptd {
 #ifndef PT_STEP_JOIN
 #define PT_STEP_JOIN 1
 #endif
+// PT_TWO_LEVEL: a BLAS internal step also takes the next level when the
+// child it continues with is internal (LaneStep).  Measured neutral (C3
+// extend 0.330 vs 0.330 ms, rank-of-8 round 0.112 vs 0.112, C5 -2 %), and
+// with a 256-byte record per pair holding both children's pairs (the
+// second level an L1 hit half the time) C3 3 % slower: off.
+#ifndef PT_TWO_LEVEL
+#define PT_TWO_LEVEL 0
+#endif
 
 // --- traversal stack: LDS columns + global spill ----------------------------
 
@@ -418,6 +426,7 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP, SE>& st,
         bool fmiss = true;
         float fT, fU, fW, TA, TB;
         uint32_t aw0, aw1, bw0, bw1;
+        uint32_t pair = L.na;   // child pair whose decision the join applies
         asm("" : "=v"(fT), "=v"(fU), "=v"(fW), "=v"(TA), "=v"(TB));
         asm("" : "=v"(aw0), "=v"(aw1), "=v"(bw0), "=v"(bw1));
         if (face) {
@@ -432,6 +441,29 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP, SE>& st,
             IntersectBoxPair(L.O, L.V, L.Y, L.Time, a0, a1, b0, b1, L.exact, TA, TB);
             aw0 = __float_as_uint(a0.w), aw1 = __float_as_uint(a1.w);
             bw0 = __float_as_uint(b0.w), bw1 = __float_as_uint(b1.w);
+#if PT_TWO_LEVEL
+            // Two levels per step: when the child the reference continues
+            // with is itself internal, its own child pair is tested in this
+            // step too -- the reference's next loop iteration, with the same
+            // Hit.Time (no face is tested in between).  The first level's
+            // set-aside child is pushed first, then the join applies the
+            // second level's decision.  Same pushes, pops and order.
+            bool g1 = TA > TB;
+            uint32_t nw0 = g1 ? bw0 : aw0, nw1 = g1 ? bw1 : aw1;
+            if ((g1 | (TA < PT_INFINITY)) & (nw1 == 0)) {
+                float Tf = g1 ? TA : TB;
+                if ((Tf < PT_INFINITY) & (L.dB < 32))
+                    st.put(L.dT + L.dB++, BlasPush<SE>(S, g1 ? aw0 : bw0, g1 ? aw1 : bw1, L.na + (g1 ? 0u : 1u)));
+                ss.node(true);
+                ss.internal();
+                pair = nw0;
+                const float4* Cp = S.mesh_nodes + 2 * (size_t)nw0;
+                float4 c0 = Cp[0], c1 = Cp[1], c2 = Cp[2], c3 = Cp[3];
+                IntersectBoxPair(L.O, L.V, L.Y, L.Time, c0, c1, c2, c3, L.exact, TA, TB);
+                aw0 = __float_as_uint(c0.w), aw1 = __float_as_uint(c1.w);
+                bw0 = __float_as_uint(c2.w), bw1 = __float_as_uint(c3.w);
+            }
+#endif
         }
         L.Time = fmiss ? L.Time : fT;
         L.Shape = fmiss ? L.Shape : 0xFFFFFFFEu;
@@ -447,7 +479,7 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP, SE>& st,
         bool push = !face & (Tfar < PT_INFINITY);
         bool moved = (face & (L.na + 1 < L.nb)) | (!face & (goB | (TA < PT_INFINITY)));
         if (push & (L.dB < 32)) {
-            st.put(L.dT + L.dB++, BlasPush<SE>(S, goB ? aw0 : bw0, goB ? aw1 : bw1, L.na + (goB ? 0u : 1u)));
+            st.put(L.dT + L.dB++, BlasPush<SE>(S, goB ? aw0 : bw0, goB ? aw1 : bw1, pair + (goB ? 0u : 1u)));
         }
         uint32_t na = face ? L.na + 1 : (goB ? bw0 : aw0);
         uint32_t nb = face ? L.nb : (goB ? bw1 : aw1);
