@@ -919,6 +919,13 @@ __global__ __launch_bounds__(256) void finalize_kernel(dscene S, uint32_t n, con
 #ifndef PT_SHADE_DIFFUSE_MINW
 #define PT_SHADE_DIFFUSE_MINW 5
 #endif
+// Occupancy floor of the other shade instantiations (metal / translucent /
+// medium code compiled in): 5 waves per SIMD (96 VGPRs, a few spills of
+// rarely live values) beat the compiler's 106-108 VGPRs at 4 waves: C5
+// shade 0.190 -> 0.179 ms, C2 0.111 -> 0.104 ms.
+#ifndef PT_SHADE_OTHER_MINW
+#define PT_SHADE_OTHER_MINW 5
+#endif
 // One tile of shade (basic_scatter.glsl:main for the tile's 256 slots).
 template <uint32_t MATS>
 PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const dparams& Pm, uint32_t tile)
@@ -1010,7 +1017,7 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
 }
 
 template <uint32_t MATS>
-__global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MINW : 1) void shade_kernel(dscene S, dslots L, dframe F,
+__global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MINW : PT_SHADE_OTHER_MINW) void shade_kernel(dscene S, dslots L, dframe F,
                                                                                     dparams Pm)
 {
     // Tiles in extend's longest-first order too: tiles with long traversals
@@ -1025,7 +1032,7 @@ __global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MIN
 // of after them, and one launch replaces two.  Same per-tile work and order
 // as extend_kernel then shade_kernel, so the results are identical.
 template <uint32_t MATS, int CAP, class E>
-__global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MINW : 1) void round_kernel(
+__global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MINW : PT_SHADE_OTHER_MINW) void round_kernel(
     dscene S, dslots L, dframe F, dparams Pm)
 {
     __shared__ E smem[CAP * 256];
