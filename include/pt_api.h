@@ -199,6 +199,12 @@ uint32_t           ptBasicRendererRunGroups(pt_basic_renderer* renderer);
  * scene allows (no spilled traversal stack).  Results are identical in every
  * mode.  Default 1, or the PT_ROUND_FUSED environment variable. */
 int                ptSetBasicRendererFusedRounds(pt_basic_renderer* renderer, int mode);
+/* OpenPBR shading (opt-in extension, no reference counterpart): 0 (default)
+ * = an OpenPBR hit ends its path with no contribution, as in the reference,
+ * whose integrator does not compile its OpenPBR BSDF (scene.glsl.inc:685);
+ * 1 = shade OpenPBR materials with the layered sampler and medium of
+ * src/scene/openpbr.glsl.inc (deviations in DESIGN.md §6). */
+int                ptSetBasicRendererOpenPBR(pt_basic_renderer* renderer, int enable);
 /* Work done since the last Reset: rays traced (one per owned pixel per round)
  * and paths completed (accumulator sample increments, basic_scatter.glsl:
  * 350-359).  Either pointer may be NULL.  Synchronises the device stream. */

@@ -149,6 +149,11 @@ PT_HD float pt_log(float x)
     return dk * 6.9313812256e-01f - ((hfsq - (s * (hfsq + R) + dk * 9.0580006145e-06f)) - f);
 }
 
+/* x^y as e^(y log x): GLSL defines pow(x, y) as exp2(y * log2(x)) (undefined
+ * for x < 0, and for x = 0 with y <= 0); the same identity in base e on the
+ * two kernels above.  x = 0, y > 0 gives e^-inf = 0. */
+PT_HD float pt_pow(float x, float y) { return pt_exp(y * pt_log(x)); }
+
 /* --- sin / cos --------------------------------------------------------------- */
 
 /* Reduce x by pi/2: returns r in [-pi/4, pi/4] and quadrant q (valid for

@@ -30,6 +30,7 @@ PT_HD pt2 operator*(pt2 a, float s) { return v2(a.x * s, a.y * s); }
 PT_HD pt2 operator*(float s, pt2 a) { return v2(s * a.x, s * a.y); }
 PT_HD pt2 operator/(pt2 a, pt2 b) { return v2(a.x / b.x, a.y / b.y); }
 PT_HD float dot(pt2 a, pt2 b) { return a.x * b.x + a.y * b.y; }
+PT_HD float length(pt2 v) { return pt_sqrt(dot(v, v)); }
 
 /* vec3 */
 PT_HD pt3 operator+(pt3 a, pt3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
@@ -69,6 +70,7 @@ PT_HD pt4 vsqrt(pt4 a) { return v4(pt_sqrt(a.x), pt_sqrt(a.y), pt_sqrt(a.z), pt_
 PT_HD pt4 vexp(pt4 a) { return v4(pt_exp(a.x), pt_exp(a.y), pt_exp(a.z), pt_exp(a.w)); }
 PT_HD pt4 vlog(pt4 a) { return v4(pt_log(a.x), pt_log(a.y), pt_log(a.z), pt_log(a.w)); }
 PT_HD pt4 vsign(pt4 a) { return v4(pt_sign(a.x), pt_sign(a.y), pt_sign(a.z), pt_sign(a.w)); }
+PT_HD pt4 vpow(pt4 a, float e) { return v4(pt_pow(a.x, e), pt_pow(a.y, e), pt_pow(a.z, e), pt_pow(a.w, e)); }
 /* max4 (src/core/common.glsl.inc:107-110) */
 PT_HD float max4(pt4 v) { return pt_max(pt_max(v.x, v.y), pt_max(v.z, v.w)); }
 

@@ -74,6 +74,34 @@ enum {
 #define PT_BASIC_TRANSLUCENT_TRANSMISSION_DEPTH   10
 #define PT_BASIC_TRANSLUCENT_SCATTERING_SPECTRUM  11
 #define PT_BASIC_TRANSLUCENT_SCATTERING_ANISOTROPY 14
+/* OpenPBR (src/scene/openpbr.glsl.inc:1-27): 64 words, two slots. */
+#define PT_OPENPBR_LAYER_BOUNCE_LIMIT                  1
+#define PT_OPENPBR_BASE_WEIGHT                         2
+#define PT_OPENPBR_BASE_SPECTRUM                       3
+#define PT_OPENPBR_BASE_SPECTRUM_TEXTURE_INDEX         6
+#define PT_OPENPBR_BASE_METALNESS                      7
+#define PT_OPENPBR_BASE_DIFFUSE_ROUGHNESS              8
+#define PT_OPENPBR_SPECULAR_WEIGHT                     9
+#define PT_OPENPBR_SPECULAR_SPECTRUM                   10
+#define PT_OPENPBR_SPECULAR_IOR                        13
+#define PT_OPENPBR_SPECULAR_ROUGHNESS                  14
+#define PT_OPENPBR_SPECULAR_ROUGHNESS_TEXTURE_INDEX    15
+#define PT_OPENPBR_SPECULAR_ROUGHNESS_ANISOTROPY       16
+#define PT_OPENPBR_TRANSMISSION_SPECTRUM               17
+#define PT_OPENPBR_TRANSMISSION_WEIGHT                 20
+#define PT_OPENPBR_TRANSMISSION_SCATTER_SPECTRUM       21
+#define PT_OPENPBR_TRANSMISSION_SCATTER_ANISOTROPY     24
+#define PT_OPENPBR_TRANSMISSION_DEPTH                  25
+#define PT_OPENPBR_TRANSMISSION_DISPERSION_ABBE_NUMBER 26
+#define PT_OPENPBR_EMISSION_SPECTRUM                   27
+#define PT_OPENPBR_EMISSION_SPECTRUM_TEXTURE_INDEX     30
+#define PT_OPENPBR_EMISSION_LUMINANCE                  31
+#define PT_OPENPBR_COAT_WEIGHT                         32
+#define PT_OPENPBR_COAT_COLOR_SPECTRUM                 33
+#define PT_OPENPBR_COAT_IOR                            36
+#define PT_OPENPBR_COAT_ROUGHNESS                      37
+#define PT_OPENPBR_COAT_ROUGHNESS_ANISOTROPY           38
+#define PT_OPENPBR_COAT_DARKENING                      39
 
 typedef struct pt_packed_transform {   /* scene.hpp:82-86 */
     float To[16];

@@ -830,16 +830,236 @@ struct context {
         return true;
     }
 
+    // --- openpbr.glsl.inc (opt-in: the reference never compiles it) ---------------
+
+    struct openpbr_parameters {                                                                     // :30-47
+        uint32_t LayerBounceLimit;
+        bool BaseIsMetal, BaseIsTranslucent, CoatIsPresent;
+        pt4 BaseReflectance;
+        float BaseDiffuseRoughness;
+        pt4 CoatRelativeIOR, CoatTransmittance;
+        pt2 CoatRoughnessAlpha;
+        float SpecularWeight;
+        pt4 SpecularRelativeIOR, SpecularReflectance;
+        pt2 SpecularRoughnessAlpha;
+        // Emission (:46, :142-152) is never read by OpenPBR_Sample: omitted.
+    };
+
+    openpbr_parameters OpenPBR_Parameters(uint32_t MI, pt2 TextureUV, pt4 Lambda, pt4 ExteriorIOR)  // :66-158
+    {
+        openpbr_parameters Parameters;
+        Parameters.CoatIsPresent = G.R01() < MaterialFloat(MI, PT_OPENPBR_COAT_WEIGHT);
+        Parameters.BaseIsMetal = G.R01() < MaterialFloat(MI, PT_OPENPBR_BASE_METALNESS);
+        Parameters.BaseIsTranslucent =
+            !Parameters.BaseIsMetal && G.R01() < MaterialFloat(MI, PT_OPENPBR_TRANSMISSION_WEIGHT);
+        Parameters.BaseReflectance = MaterialFloat(MI, PT_OPENPBR_BASE_WEIGHT) *
+                                     SampleParametricSpectrum(MaterialVec3(MI, PT_OPENPBR_BASE_SPECTRUM), Lambda);
+        Parameters.BaseDiffuseRoughness = MaterialFloat(MI, PT_OPENPBR_BASE_DIFFUSE_ROUGHNESS);
+        uint32_t BaseSpectrumTextureIndex = MaterialUint(MI, PT_OPENPBR_BASE_SPECTRUM_TEXTURE_INDEX);
+        if (BaseSpectrumTextureIndex != TEXTURE_INDEX_NONE) {
+            pt4 Value = SampleTexture(BaseSpectrumTextureIndex, TextureUV);
+            Parameters.BaseReflectance =
+                Parameters.BaseReflectance * SampleParametricSpectrum(v3(Value.x, Value.y, Value.z), Lambda);
+        }
+        // (unused without a coat; set so that the struct is fully defined)
+        Parameters.CoatRelativeIOR = v4s(1.0f);
+        Parameters.CoatTransmittance = v4s(1.0f);
+        Parameters.CoatRoughnessAlpha = v2(0.0f, 0.0f);
+        if (Parameters.CoatIsPresent) {
+            Parameters.CoatRelativeIOR = ExteriorIOR / MaterialFloat(MI, PT_OPENPBR_COAT_IOR);
+            Parameters.CoatTransmittance = SampleParametricSpectrum(MaterialVec3(MI, PT_OPENPBR_COAT_COLOR_SPECTRUM), Lambda);
+            Parameters.CoatRoughnessAlpha = GGXRoughnessAlpha(MaterialFloat(MI, PT_OPENPBR_COAT_ROUGHNESS),
+                                                              MaterialFloat(MI, PT_OPENPBR_COAT_ROUGHNESS_ANISOTROPY));
+        }
+        Parameters.SpecularWeight = MaterialFloat(MI, PT_OPENPBR_SPECULAR_WEIGHT);
+        Parameters.SpecularReflectance = SampleParametricSpectrum(MaterialVec3(MI, PT_OPENPBR_SPECULAR_SPECTRUM), Lambda);
+        pt4 SpecularIOR = CauchyEmpiricalIOR(MaterialFloat(MI, PT_OPENPBR_SPECULAR_IOR),
+                                             MaterialFloat(MI, PT_OPENPBR_TRANSMISSION_DISPERSION_ABBE_NUMBER), Lambda);
+        if (Parameters.CoatIsPresent)
+            Parameters.SpecularRelativeIOR = MaterialFloat(MI, PT_OPENPBR_COAT_IOR) / SpecularIOR;
+        else
+            Parameters.SpecularRelativeIOR = ExteriorIOR / SpecularIOR;
+        float SpecularRoughness = MaterialFloat(MI, PT_OPENPBR_SPECULAR_ROUGHNESS);
+        uint32_t SpecularRoughnessTextureIndex = MaterialUint(MI, PT_OPENPBR_SPECULAR_ROUGHNESS_TEXTURE_INDEX);
+        if (SpecularRoughnessTextureIndex != TEXTURE_INDEX_NONE) {
+            pt4 Value = SampleTexture(SpecularRoughnessTextureIndex, TextureUV);
+            SpecularRoughness *= Value.x;
+        }
+        Parameters.SpecularRoughnessAlpha =
+            GGXRoughnessAlpha(SpecularRoughness, MaterialFloat(MI, PT_OPENPBR_SPECULAR_ROUGHNESS_ANISOTROPY));
+        Parameters.LayerBounceLimit = MaterialUint(MI, PT_OPENPBR_LAYER_BOUNCE_LIMIT);
+        return Parameters;
+    }
+
+    void OpenPBR_Medium(uint32_t MI, pt4 Lambda, medium& Medium)                                    // :160-191
+    {
+        Medium.IOR = CauchyEmpiricalIOR(MaterialFloat(MI, PT_OPENPBR_SPECULAR_IOR),
+                                        MaterialFloat(MI, PT_OPENPBR_TRANSMISSION_DISPERSION_ABBE_NUMBER), Lambda);
+        float TransmissionDepth = MaterialFloat(MI, PT_OPENPBR_TRANSMISSION_DEPTH);
+        if (TransmissionDepth > 0.0f) {
+            pt4 ExtinctionRate =
+                -vlog(SampleParametricSpectrum(MaterialVec3(MI, PT_OPENPBR_TRANSMISSION_SPECTRUM), Lambda)) / TransmissionDepth;
+            pt4 ScatteringRate =
+                SampleParametricSpectrum(MaterialVec3(MI, PT_OPENPBR_TRANSMISSION_SCATTER_SPECTRUM), Lambda) / TransmissionDepth;
+            Medium.AbsorptionRate = vmax(ExtinctionRate - ScatteringRate, 0.0f);
+            Medium.ScatteringRate = ScatteringRate;
+            Medium.ScatteringAnisotropy = MaterialFloat(MI, PT_OPENPBR_TRANSMISSION_SCATTER_ANISOTROPY);
+        } else {
+            Medium.AbsorptionRate = v4s(0.0f);
+            Medium.ScatteringRate = v4s(0.0f);
+            Medium.ScatteringAnisotropy = 0.0f;
+        }
+    }
+
+    void OpenPBR_CoatSample(const openpbr_parameters& Parameters, pt3 Out, pt3& In, pt4& PathThroughput,  // :194-283
+                            pt4& PathDensity)
+    {
+        if (!Parameters.CoatIsPresent) { In = -Out; return; }
+        float NormalU1 = G.R01();
+        float NormalU2 = G.R01();
+        pt3 Normal = GGXVisibleNormal(Out * pt_sign(Out.z), Parameters.CoatRoughnessAlpha, NormalU1, NormalU2);
+        float Cosine = dot(Normal, Out);
+        pt4 RelativeIOR = Parameters.CoatRelativeIOR;
+        if (Out.z < 0) RelativeIOR = 1.0f / RelativeIOR;
+        float RefractedCosineSquared = 1 - RelativeIOR.x * RelativeIOR.x * (1 - Cosine * Cosine);
+        float RefractedCosine = -pt_sign(Out.z) * pt_sqrt(pt_max(RefractedCosineSquared, 0.0f));
+        // :227 passes (RefractedCosine, Cosine, RelativeIOR.x) to
+        // FresnelDielectric(Eta, CosTheta1, CosTheta2); restated in signature
+        // order, as the base layer calls it (:346).
+        float Reflectance = FresnelDielectric(RelativeIOR.x, Cosine, RefractedCosine);
+        if (G.R01() < Reflectance) {
+            In = 2 * Cosine * Normal - Out;
+            if (In.z * Out.z <= 0) { PathDensity = v4s(0.0f); return; }
+            PathThroughput = PathThroughput * GGXSmithG1(In, Parameters.CoatRoughnessAlpha);
+            if (Out.z < 0) {
+                float Exponent = -(0.5f / Out.z + 0.5f / In.z);
+                PathThroughput = PathThroughput * vpow(Parameters.CoatTransmittance, Exponent);
+            }
+        } else {
+            In = (RelativeIOR.x * Cosine + RefractedCosine) * Normal - RelativeIOR.x * Out;
+            if (In.z * Out.z > 0) { PathDensity = v4s(0.0f); return; }
+            PathThroughput = PathThroughput * GGXSmithG1(In, Parameters.CoatRoughnessAlpha);
+            if (Out.z < 0)
+                PathThroughput = PathThroughput * vpow(Parameters.CoatTransmittance, -0.5f / Out.z);
+            else
+                PathThroughput = PathThroughput * vpow(Parameters.CoatTransmittance, -0.5f / In.z);
+        }
+    }
+
+    void OpenPBR_BaseSpecularSample(const openpbr_parameters& Parameters, pt3 Out, pt3& In,           // :286-435
+                                    pt4& PathThroughput, pt4& PathDensity)
+    {
+        float NormalU1 = G.R01();
+        float NormalU2 = G.R01();
+        pt3 Normal = GGXVisibleNormal(Out * pt_sign(Out.z), Parameters.SpecularRoughnessAlpha, NormalU1, NormalU2);
+        float Cosine = dot(Normal, Out);
+        if (Parameters.BaseIsMetal) {
+            In = 2 * Cosine * Normal - Out;
+            if (Out.z * In.z <= 0) { PathDensity = v4s(0.0f); return; }
+            float Shadowing = GGXSmithG1(Out, Parameters.SpecularRoughnessAlpha);
+            pt4 Fresnel = Parameters.SpecularWeight *
+                          SchlickFresnelMetal(Parameters.BaseReflectance, Parameters.SpecularReflectance, pt_abs(Cosine));
+            PathThroughput = PathThroughput * (Fresnel * Shadowing);
+        } else {
+            pt4 RelativeIOR = Parameters.SpecularRelativeIOR;
+            if (Out.z < 0) RelativeIOR = 1.0f / RelativeIOR;
+            if (Parameters.SpecularWeight < 1.0f) {
+                pt4 R = pt_sqrt(Parameters.SpecularWeight) * (1.0f - RelativeIOR) / (1.0f + RelativeIOR);
+                RelativeIOR = (1.0f - R) / (1.0f + R);
+            }
+            float RefractedCosine = ComputeCosThetaRefracted(RelativeIOR.x, Cosine);
+            float Reflectance = FresnelDielectric(RelativeIOR.x, Cosine, RefractedCosine);
+            if (G.R01() < Reflectance) {
+                In = 2 * Cosine * Normal - Out;
+                if (In.z * Out.z <= 0) { PathDensity = v4s(0.0f); return; }
+                if (Out.z > 0) PathThroughput = PathThroughput * Parameters.SpecularReflectance;
+                PathThroughput = PathThroughput * GGXSmithG1(In, Parameters.SpecularRoughnessAlpha);
+            } else {
+                In = (RelativeIOR.x * Cosine + RefractedCosine) * Normal - RelativeIOR.x * Out;
+                if (In.z * Out.z > 0) { PathDensity = v4s(0.0f); return; }
+                float Shadowing = GGXSmithG1(In, Parameters.SpecularRoughnessAlpha);
+                if (length(Parameters.SpecularRoughnessAlpha) > PT_EPSILON) {
+                    pt4 Fresnel = v4s(0.0f);   // :390-391 "TODO: This is broken for now!"
+                    pt3 Normal2 = SafeNormalize(In + Out * RelativeIOR.y);
+                    pt3 Normal3 = SafeNormalize(In + Out * RelativeIOR.z);
+                    pt3 Normal4 = SafeNormalize(In + Out * RelativeIOR.w);
+                    pt4 Density = v4s(0.0f);
+                    Density.x = GGXDistribution(Normal, Parameters.SpecularRoughnessAlpha);
+                    if (dot(In, Normal2) * dot(Out, Normal2) < 0.0f)
+                        Density.y = GGXDistribution(Normal2, Parameters.SpecularRoughnessAlpha);
+                    if (dot(In, Normal3) * dot(Out, Normal3) < 0.0f)
+                        Density.z = GGXDistribution(Normal3, Parameters.SpecularRoughnessAlpha);
+                    if (dot(In, Normal4) * dot(Out, Normal4) < 0.0f)
+                        Density.w = GGXDistribution(Normal4, Parameters.SpecularRoughnessAlpha);
+                    Density = Density / pt_max(PT_EPSILON, max4(Density));
+                    PathThroughput = PathThroughput * (Density * Fresnel * Shadowing);
+                    PathDensity = PathDensity * (Density * Fresnel);
+                } else {
+                    PathThroughput = PathThroughput * v4(Shadowing, 0, 0, 0);
+                    PathDensity = PathDensity * v4(1, 0, 0, 0);
+                }
+            }
+        }
+    }
+
+    void OpenPBR_BaseDiffuseSample(const openpbr_parameters& Parameters, pt3 Out, pt3& In,            // :438-461
+                                   pt4& PathThroughput)
+    {
+        if (Parameters.BaseIsTranslucent) { In = -Out; return; }
+        In = SafeNormalize(RandomDirection(G) + v3(0, 0, 1));
+        float S_ = dot(In, Out) - In.z * Out.z;
+        float T_ = S_ > 0 ? pt_max(In.z, Out.z) : 1.0f;
+        float SigmaSq = Parameters.BaseDiffuseRoughness * Parameters.BaseDiffuseRoughness;
+        pt4 A = (1 - 0.5f * SigmaSq / (SigmaSq + 0.33f)) + 0.17f * Parameters.BaseReflectance * SigmaSq / (SigmaSq + 0.13f);
+        float B = 0.45f * SigmaSq / (SigmaSq + 0.09f);
+        PathThroughput = PathThroughput * (Parameters.BaseReflectance * (B * S_ / T_ + A));
+    }
+
+    bool OpenPBR_Sample(const openpbr_parameters& Parameters, pt3 Out, pt3& In, pt4& Throughput,       // :463-515
+                        pt4& InPDF)
+    {
+        const int LAYER_EXTERNAL = -1, LAYER_COAT = 0, LAYER_BASE_SPECULAR = 1, LAYER_BASE_DIFFUSE = 2;
+        int Layer;
+        if (Out.z > 0) Layer = Parameters.CoatIsPresent ? LAYER_COAT : LAYER_BASE_SPECULAR;
+        else Layer = LAYER_BASE_SPECULAR;
+        Throughput = v4s(1.0f);
+        InPDF = v4s(1.0f);
+        In = -Out;   // the reference leaves In unassigned when LayerBounceLimit is 0
+        for (uint32_t I = 0; I < Parameters.LayerBounceLimit; I++) {
+            if (Layer == LAYER_COAT) {
+                OpenPBR_CoatSample(Parameters, Out, In, Throughput, InPDF);
+                Layer = In.z < 0 ? LAYER_BASE_SPECULAR : LAYER_EXTERNAL;
+            } else if (Layer == LAYER_BASE_SPECULAR) {
+                OpenPBR_BaseSpecularSample(Parameters, Out, In, Throughput, InPDF);
+                Layer = In.z < 0 ? LAYER_BASE_DIFFUSE : LAYER_COAT;
+            } else if (Layer == LAYER_BASE_DIFFUSE) {
+                OpenPBR_BaseDiffuseSample(Parameters, Out, In, Throughput);
+                Layer = In.z < 0 ? LAYER_EXTERNAL : LAYER_BASE_SPECULAR;
+            } else if (Layer == LAYER_EXTERNAL) {
+                break;
+            }
+            if (max4(InPDF) < PT_EPSILON) return false;
+            Out = -In;
+        }
+        return true;
+    }
+
     // Dispatch (scene.glsl.inc:687-762).  OpenPBR / unknown types are not
     // compiled into the reference kernels: Sample/Evaluate return false,
     // HasDirac false; LoadMedium leaves the medium as the vacuum (the
-    // reference's `out` parameter is undefined there).
+    // reference's `out` parameter is undefined there).  With OpenPBR shading
+    // enabled (the renderer's opt-in), OpenPBR is a sampling-only BSDF:
+    // HasDirac true (no skybox light sampling), SampleBSDF = OpenPBR_Parameters
+    // + OpenPBR_Sample, LoadMedium = OpenPBR_Medium.
+    bool OpenPBR = false;
+
     bool MaterialLoadMedium(uint32_t M, pt4 Lambda, medium& Medium)
     {
         Medium.IOR = v4s(1.0f); Medium.AbsorptionRate = v4s(0.0f); Medium.ScatteringRate = v4s(0.0f);
         Medium.ScatteringAnisotropy = 0.0f;
         uint32_t Type = MaterialType(M);
         if (Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT) return BasicTranslucent_LoadMedium(M, Lambda, Medium);
+        if (Type == PT_MATERIAL_TYPE_OPENPBR && OpenPBR) { OpenPBR_Medium(M, Lambda, Medium); return true; }
         return false;
     }
     bool MaterialHasDiracBSDF(const bsdf_parameters& P)
@@ -848,6 +1068,7 @@ struct context {
         if (Type == PT_MATERIAL_TYPE_BASIC_DIFFUSE) return false;
         if (Type == PT_MATERIAL_TYPE_BASIC_METAL) return BasicMetal_HasDiracBSDF(P);
         if (Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT) return BasicTranslucent_HasDiracBSDF(P);
+        if (Type == PT_MATERIAL_TYPE_OPENPBR) return OpenPBR;
         return false;
     }
     bool MaterialEvaluateBSDF(const bsdf_parameters& P, pt3 In, pt3 Out, pt4& T, pt4& Pr)
@@ -864,6 +1085,10 @@ struct context {
         if (Type == PT_MATERIAL_TYPE_BASIC_DIFFUSE) return BasicDiffuse_SampleBSDF(P, In, Out, T, Pr);
         if (Type == PT_MATERIAL_TYPE_BASIC_METAL) return BasicMetal_SampleBSDF(P, In, Out, T, Pr);
         if (Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT) return BasicTranslucent_SampleBSDF(P, In, Out, T, Pr);
+        if (Type == PT_MATERIAL_TYPE_OPENPBR && OpenPBR) {
+            openpbr_parameters Q = OpenPBR_Parameters(P.MaterialIndex, P.TextureUV, P.Lambda, P.ExteriorIOR);
+            return OpenPBR_Sample(Q, In, Out, T, Pr);
+        }
         return false;
     }
 
@@ -1031,6 +1256,7 @@ struct oracle_renderer {
     uint32_t W, H, Rank, NRanks;
     int Threads;
     pt_basic_renderer_params Params{};
+    bool OpenPBR = false;                  // oracle_set_openpbr
     std::vector<uint32_t> Pixels;          // owned pixel indices (y*W+x)
     std::vector<pixel_state> State;        // parallel to Pixels
     std::vector<float> Accum;              // W*H*4
@@ -1146,6 +1372,7 @@ struct oracle_renderer {
         ParallelFor(Pixels.size(), [&](size_t i) {
             context C(Scene);
             C.PathTerminationProbability = Params.PathTerminationProbability;
+            C.OpenPBR = OpenPBR;
             uint32_t pix = Pixels[i];
             int X = (int)(pix % W), Y = (int)(pix / W);
             C.G.State = pt_seed((uint32_t)X, (uint32_t)Y, Seed);
@@ -1214,6 +1441,7 @@ oracle_renderer* oracle_create(const pt_scene_packs* packs, uint32_t width, uint
 
 void oracle_destroy(oracle_renderer* r) { delete r; }
 pt_basic_renderer_params* oracle_params(oracle_renderer* r) { return &r->Params; }
+void oracle_set_openpbr(oracle_renderer* r, int enable) { r->OpenPBR = enable != 0; }
 
 // ResetBasicRenderer (basic.cpp:285-304): one scatter dispatch, Restart=1,
 // seeded with the current FrameIndex.

@@ -28,6 +28,8 @@ oracle_renderer* oracle_create(const pt_scene_packs* packs, uint32_t width, uint
                                uint32_t rank, uint32_t nranks, int threads);
 void oracle_destroy(oracle_renderer* r);
 pt_basic_renderer_params* oracle_params(oracle_renderer* r);
+/* OpenPBR shading on/off (ptSetBasicRendererOpenPBR); off by default. */
+void oracle_set_openpbr(oracle_renderer* r, int enable);
 void oracle_reset(oracle_renderer* r);
 void oracle_run(oracle_renderer* r, uint32_t rounds);
 void oracle_read_accum(oracle_renderer* r, float* rgba);

@@ -234,6 +234,7 @@ HIP_API = {
     "ptBasicRendererSlotCount": (_u32, [_vp]),
     "ptBasicRendererRunGroups": (_u32, [_vp]),
     "ptSetBasicRendererFusedRounds": (_i32, [_vp, _i32]),
+    "ptSetBasicRendererOpenPBR": (_i32, [_vp, _i32]),
     "ptGetStats": (_i32, [_vp, _vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "ptReadBasicRendererState": (_i32, [_vp, _vp, _vp]),
     "ptTraceRays": (_i32, [_vp, _vp, _u32, _fptr, _u32ptr, _fptr, _vp]),

@@ -220,17 +220,224 @@ PT_DEV bool Translucent_Sample(const dscene& S, rng& G, const bsdf_parameters& P
     return true;
 }
 
+// --- OpenPBR (src/scene/openpbr.glsl.inc) ----------------------------------------
+// The reference packs OpenPBR materials but never shades them (its include is
+// commented out, scene.glsl.inc:685, and DISPATCH_MATERIAL has no OpenPBR
+// case), so by default an OpenPBR hit ends the path as there.  With
+// ptSetBasicRendererOpenPBR the layered sampler below is dispatched instead
+// (PT_MATS_OPENPBR instantiation): a sampling-only BSDF (HasDirac true, so no
+// skybox light sampling), the medium of openpbr.glsl.inc:160-191.  Deviations
+// from the uncompiled text: the coat's FresnelDielectric
+// arguments are put in signature order; Emission, computed but never read by
+// OpenPBR_Sample, is not evaluated; a LayerBounceLimit of 0 leaves In = -Out
+// (the reference's out parameter is unassigned).
+
+struct openpbr_parameters {                       // openpbr.glsl.inc:30-47
+    uint32_t LayerBounceLimit;
+    bool BaseIsMetal, BaseIsTranslucent, CoatIsPresent;
+    pt4 BaseReflectance;
+    float BaseDiffuseRoughness;
+    pt4 CoatRelativeIOR, CoatTransmittance;
+    pt2 CoatRoughnessAlpha;
+    float SpecularWeight;
+    pt4 SpecularRelativeIOR, SpecularReflectance;
+    pt2 SpecularRoughnessAlpha;
+};
+
+// OpenPBR_Parameters (:66-158): three stochastic layer choices, then the
+// spectral parameters at the cluster wavelengths.
+PT_DEV openpbr_parameters OpenPBR_Parameters(const dscene& S, rng& G, const bsdf_parameters& P)
+{
+    const uint32_t M = P.MaterialIndex;
+    openpbr_parameters Q;
+    Q.CoatIsPresent = G.R01() < MFloat(S, M, PT_OPENPBR_COAT_WEIGHT);
+    Q.BaseIsMetal = G.R01() < MFloat(S, M, PT_OPENPBR_BASE_METALNESS);
+    Q.BaseIsTranslucent = !Q.BaseIsMetal && G.R01() < MFloat(S, M, PT_OPENPBR_TRANSMISSION_WEIGHT);
+    Q.BaseReflectance = MFloat(S, M, PT_OPENPBR_BASE_WEIGHT) *
+                        SampleParametricSpectrum(MVec3(S, M, PT_OPENPBR_BASE_SPECTRUM), P.Lambda);
+    Q.BaseDiffuseRoughness = MFloat(S, M, PT_OPENPBR_BASE_DIFFUSE_ROUGHNESS);
+    uint32_t Tx = MUint(S, M, PT_OPENPBR_BASE_SPECTRUM_TEXTURE_INDEX);
+    if (Tx != TEXTURE_INDEX_NONE) {
+        pt4 V = SampleTexture(S, Tx, P.TextureUV);
+        Q.BaseReflectance = Q.BaseReflectance * SampleParametricSpectrum(v3(V.x, V.y, V.z), P.Lambda);
+    }
+    const float CoatIOR = MFloat(S, M, PT_OPENPBR_COAT_IOR);
+    Q.CoatRelativeIOR = v4s(1.0f); Q.CoatTransmittance = v4s(1.0f); Q.CoatRoughnessAlpha = v2(0.0f, 0.0f);
+    if (Q.CoatIsPresent) {
+        Q.CoatRelativeIOR = P.ExteriorIOR / CoatIOR;
+        Q.CoatTransmittance = SampleParametricSpectrum(MVec3(S, M, PT_OPENPBR_COAT_COLOR_SPECTRUM), P.Lambda);
+        Q.CoatRoughnessAlpha = GGXRoughnessAlpha(MFloat(S, M, PT_OPENPBR_COAT_ROUGHNESS),
+                                                 MFloat(S, M, PT_OPENPBR_COAT_ROUGHNESS_ANISOTROPY));
+    }
+    Q.SpecularWeight = MFloat(S, M, PT_OPENPBR_SPECULAR_WEIGHT);
+    Q.SpecularReflectance = SampleParametricSpectrum(MVec3(S, M, PT_OPENPBR_SPECULAR_SPECTRUM), P.Lambda);
+    pt4 SpecularIOR = CauchyEmpiricalIOR(MFloat(S, M, PT_OPENPBR_SPECULAR_IOR),
+                                         MFloat(S, M, PT_OPENPBR_TRANSMISSION_DISPERSION_ABBE_NUMBER), P.Lambda);
+    Q.SpecularRelativeIOR = Q.CoatIsPresent ? CoatIOR / SpecularIOR : P.ExteriorIOR / SpecularIOR;
+    float SpecularRoughness = MFloat(S, M, PT_OPENPBR_SPECULAR_ROUGHNESS);
+    Tx = MUint(S, M, PT_OPENPBR_SPECULAR_ROUGHNESS_TEXTURE_INDEX);
+    if (Tx != TEXTURE_INDEX_NONE) SpecularRoughness = SpecularRoughness * SampleTexture(S, Tx, P.TextureUV).x;
+    Q.SpecularRoughnessAlpha = GGXRoughnessAlpha(SpecularRoughness, MFloat(S, M, PT_OPENPBR_SPECULAR_ROUGHNESS_ANISOTROPY));
+    Q.LayerBounceLimit = MUint(S, M, PT_OPENPBR_LAYER_BOUNCE_LIMIT);
+    return Q;
+}
+
+// OpenPBR_Medium (:160-191)
+PT_DEV void OpenPBR_Medium(const dscene& S, uint32_t M, pt4 Lambda, medium& Md)
+{
+    Md.IOR = CauchyEmpiricalIOR(MFloat(S, M, PT_OPENPBR_SPECULAR_IOR),
+                                MFloat(S, M, PT_OPENPBR_TRANSMISSION_DISPERSION_ABBE_NUMBER), Lambda);
+    float TD = MFloat(S, M, PT_OPENPBR_TRANSMISSION_DEPTH);
+    if (TD > 0.0f) {
+        pt4 Ext = -vlog(SampleParametricSpectrum(MVec3(S, M, PT_OPENPBR_TRANSMISSION_SPECTRUM), Lambda)) / TD;
+        pt4 Sc = SampleParametricSpectrum(MVec3(S, M, PT_OPENPBR_TRANSMISSION_SCATTER_SPECTRUM), Lambda) / TD;
+        Md.AbsorptionRate = vmax(Ext - Sc, 0.0f);
+        Md.ScatteringRate = Sc;
+        Md.ScatteringAnisotropy = MFloat(S, M, PT_OPENPBR_TRANSMISSION_SCATTER_ANISOTROPY);
+    } else {
+        Md.AbsorptionRate = v4s(0.0f);
+        Md.ScatteringRate = v4s(0.0f);
+        Md.ScatteringAnisotropy = 0.0f;
+    }
+}
+
+// OpenPBR_CoatSample (:194-283)
+PT_DEV void OpenPBR_CoatSample(rng& G, const openpbr_parameters& Q, pt3 Out, pt3& In, pt4& T, pt4& D)
+{
+    if (!Q.CoatIsPresent) { In = -Out; return; }
+    float U1 = G.R01();
+    float U2 = G.R01();
+    pt3 N = GGXVisibleNormal(Out * pt_sign(Out.z), Q.CoatRoughnessAlpha, U1, U2);
+    float Cosine = dot(N, Out);
+    pt4 R = Q.CoatRelativeIOR;
+    if (Out.z < 0) R = 1.0f / R;
+    float RefractedCosineSquared = 1 - R.x * R.x * (1 - Cosine * Cosine);
+    float RefractedCosine = -pt_sign(Out.z) * pt_sqrt(pt_max(RefractedCosineSquared, 0.0f));
+    float Reflectance = FresnelDielectric(R.x, Cosine, RefractedCosine);
+    if (G.R01() < Reflectance) {
+        In = 2 * Cosine * N - Out;
+        if (In.z * Out.z <= 0) { D = v4s(0.0f); return; }
+        T = T * GGXSmithG1(In, Q.CoatRoughnessAlpha);
+        if (Out.z < 0) {
+            float Exponent = -(0.5f / Out.z + 0.5f / In.z);
+            T = T * vpow(Q.CoatTransmittance, Exponent);
+        }
+    } else {
+        In = (R.x * Cosine + RefractedCosine) * N - R.x * Out;
+        if (In.z * Out.z > 0) { D = v4s(0.0f); return; }
+        T = T * GGXSmithG1(In, Q.CoatRoughnessAlpha);
+        if (Out.z < 0) T = T * vpow(Q.CoatTransmittance, -0.5f / Out.z);
+        else T = T * vpow(Q.CoatTransmittance, -0.5f / In.z);
+    }
+}
+
+// OpenPBR_BaseSpecularSample (:286-435)
+PT_DEV void OpenPBR_BaseSpecularSample(rng& G, const openpbr_parameters& Q, pt3 Out, pt3& In, pt4& T, pt4& D)
+{
+    const pt2 A = Q.SpecularRoughnessAlpha;
+    float U1 = G.R01();
+    float U2 = G.R01();
+    pt3 N = GGXVisibleNormal(Out * pt_sign(Out.z), A, U1, U2);
+    float Cosine = dot(N, Out);
+    if (Q.BaseIsMetal) {
+        In = 2 * Cosine * N - Out;
+        if (Out.z * In.z <= 0) { D = v4s(0.0f); return; }
+        float Shadowing = GGXSmithG1(Out, A);
+        pt4 F = Q.SpecularWeight * SchlickFresnelMetal(Q.BaseReflectance, Q.SpecularReflectance, pt_abs(Cosine));
+        T = T * (F * Shadowing);
+        return;
+    }
+    pt4 R = Q.SpecularRelativeIOR;
+    if (Out.z < 0) R = 1.0f / R;
+    if (Q.SpecularWeight < 1.0f) {
+        pt4 Rw = pt_sqrt(Q.SpecularWeight) * (1.0f - R) / (1.0f + R);
+        R = (1.0f - Rw) / (1.0f + Rw);
+    }
+    float RefractedCosine = ComputeCosThetaRefracted(R.x, Cosine);
+    float Reflectance = FresnelDielectric(R.x, Cosine, RefractedCosine);
+    if (G.R01() < Reflectance) {
+        In = 2 * Cosine * N - Out;
+        if (In.z * Out.z <= 0) { D = v4s(0.0f); return; }
+        if (Out.z > 0) T = T * Q.SpecularReflectance;
+        T = T * GGXSmithG1(In, A);
+        return;
+    }
+    In = (R.x * Cosine + RefractedCosine) * N - R.x * Out;
+    if (In.z * Out.z > 0) { D = v4s(0.0f); return; }
+    float Shadowing = GGXSmithG1(In, A);
+    if (length(A) > PT_EPSILON) {
+        pt4 F = v4s(0.0f);   // the reference's "TODO: This is broken for now!" (:390-391)
+        pt3 N2 = SafeNormalize(In + Out * R.y);
+        pt3 N3 = SafeNormalize(In + Out * R.z);
+        pt3 N4 = SafeNormalize(In + Out * R.w);
+        pt4 Dn = v4s(0.0f);
+        Dn.x = GGXDistribution(N, A);
+        if (dot(In, N2) * dot(Out, N2) < 0.0f) Dn.y = GGXDistribution(N2, A);
+        if (dot(In, N3) * dot(Out, N3) < 0.0f) Dn.z = GGXDistribution(N3, A);
+        if (dot(In, N4) * dot(Out, N4) < 0.0f) Dn.w = GGXDistribution(N4, A);
+        Dn = Dn / pt_max(PT_EPSILON, max4(Dn));
+        T = T * (Dn * F * Shadowing);
+        D = D * (Dn * F);
+    } else {
+        T = T * v4(Shadowing, 0, 0, 0);
+        D = D * v4(1, 0, 0, 0);
+    }
+}
+
+// OpenPBR_BaseDiffuseSample (:438-461): Oren-Nayar-weighted cosine sampling.
+PT_DEV void OpenPBR_BaseDiffuseSample(rng& G, const openpbr_parameters& Q, pt3 Out, pt3& In, pt4& T)
+{
+    if (Q.BaseIsTranslucent) { In = -Out; return; }
+    In = SafeNormalize(RandomDirection(G) + v3(0, 0, 1));
+    float Sv = dot(In, Out) - In.z * Out.z;
+    float Tv = Sv > 0 ? pt_max(In.z, Out.z) : 1.0f;
+    float SigmaSq = Q.BaseDiffuseRoughness * Q.BaseDiffuseRoughness;
+    pt4 A = (1 - 0.5f * SigmaSq / (SigmaSq + 0.33f)) + 0.17f * Q.BaseReflectance * SigmaSq / (SigmaSq + 0.13f);
+    float B = 0.45f * SigmaSq / (SigmaSq + 0.09f);
+    T = T * (Q.BaseReflectance * (B * Sv / Tv + A));
+}
+
+// OpenPBR_Sample (:463-515): a random walk through the layer stack.
+PT_DEV bool OpenPBR_Sample(rng& G, const openpbr_parameters& Q, pt3 Out, pt3& In, pt4& T, pt4& D)
+{
+    enum { EXTERNAL = -1, COAT = 0, BASE_SPECULAR = 1, BASE_DIFFUSE = 2 };
+    int Layer = (Out.z > 0 && Q.CoatIsPresent) ? COAT : BASE_SPECULAR;
+    T = v4s(1.0f);
+    D = v4s(1.0f);
+    In = -Out;
+    for (uint32_t I = 0; I < Q.LayerBounceLimit; I++) {
+        if (Layer == COAT) {
+            OpenPBR_CoatSample(G, Q, Out, In, T, D);
+            Layer = In.z < 0 ? BASE_SPECULAR : EXTERNAL;
+        } else if (Layer == BASE_SPECULAR) {
+            OpenPBR_BaseSpecularSample(G, Q, Out, In, T, D);
+            Layer = In.z < 0 ? BASE_DIFFUSE : COAT;
+        } else if (Layer == BASE_DIFFUSE) {
+            OpenPBR_BaseDiffuseSample(G, Q, Out, In, T);
+            Layer = In.z < 0 ? EXTERNAL : BASE_SPECULAR;
+        } else {
+            break;
+        }
+        if (max4(D) < PT_EPSILON) return false;
+        Out = -In;
+    }
+    return true;
+}
+
 // Material-type specialisation of the shade kernel: MATS is a superset of the
 // types referenced by the scene's shapes (computed on the host at upload), so
 // dispatch branches for absent types are compiled out without changing any
 // result.  PT_MATS_SCATTER: some medium can scatter (SceneScatterRate > 0 or
-// a translucent material exists).
+// a translucent / shaded OpenPBR material exists).  PT_MATS_OPENPBR: OpenPBR
+// shading is enabled and the scene has OpenPBR shapes.
 template <uint32_t MATS>
 PT_DEV void LoadMedium(const dscene& S, uint32_t M, pt4 Lambda, medium& Md)
 {
     Md.IOR = v4s(1.0f); Md.AbsorptionRate = v4s(0.0f); Md.ScatteringRate = v4s(0.0f); Md.ScatteringAnisotropy = 0.0f;
-    if (!(MATS & PT_MATS_TRANSLUCENT)) return;
-    if (MUint(S, M, 0) != PT_MATERIAL_TYPE_BASIC_TRANSLUCENT) return;
+    if (!(MATS & (PT_MATS_TRANSLUCENT | PT_MATS_OPENPBR))) return;
+    uint32_t Type = MUint(S, M, 0);
+    if ((MATS & PT_MATS_OPENPBR) && Type == PT_MATERIAL_TYPE_OPENPBR) { OpenPBR_Medium(S, M, Lambda, Md); return; }
+    if (!(MATS & PT_MATS_TRANSLUCENT) || Type != PT_MATERIAL_TYPE_BASIC_TRANSLUCENT) return;
     Md.IOR = CauchyEmpiricalIOR(MFloat(S, M, PT_BASIC_TRANSLUCENT_IOR), MFloat(S, M, PT_BASIC_TRANSLUCENT_ABBE_NUMBER), Lambda);
     float TD = MFloat(S, M, PT_BASIC_TRANSLUCENT_TRANSMISSION_DEPTH);
     if (TD > 0.0f) {
@@ -266,6 +473,7 @@ PT_DEV bool HasDirac(const dscene& S, const bsdf_parameters& P, uint32_t Type)
         return MaterialTexturableValue(S, P.MaterialIndex, PT_BASIC_METAL_ROUGHNESS, P.TextureUV) < 1e-3f;
     if ((MATS & PT_MATS_TRANSLUCENT) && Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT)
         return MaterialTexturableValue(S, P.MaterialIndex, PT_BASIC_TRANSLUCENT_ROUGHNESS, P.TextureUV) < 1e-3f;
+    if ((MATS & PT_MATS_OPENPBR) && Type == PT_MATERIAL_TYPE_OPENPBR) return true;   // sampling only
     return false;
 }
 
@@ -301,6 +509,9 @@ PT_DEV bool SampleSurfaceIntegrand(const dscene& S, rng& G, pt3 Nrm, pt3 TX, pt3
             ok = Metal_Sample(S, G, P, Out, In, Throughput, MaterialPDF);
         } else if ((MATS & PT_MATS_TRANSLUCENT) && Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT) {
             ok = Translucent_Sample(S, G, P, Out, In, Throughput, MaterialPDF);
+        } else if ((MATS & PT_MATS_OPENPBR) && Type == PT_MATERIAL_TYPE_OPENPBR) {
+            openpbr_parameters Q = OpenPBR_Parameters(S, G, P);
+            ok = OpenPBR_Sample(G, Q, Out, In, Throughput, MaterialPDF);
         } else {
             ok = false;
         }
@@ -504,9 +715,9 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
     for (int I = 0; I < 4; I++) Active = pt_umin(Active, Path.Active[I]);
 
     medium Md = ResolveMedium<MATS>(S, Active, Lambda);
-    // Without translucent materials every medium is vacuum: exp(-0 * t) = 1
+    // Without translucent (or shaded OpenPBR) materials every medium is vacuum: exp(-0 * t) = 1
     // exactly, so the multiply is an identity and is skipped.
-    if (MATS & PT_MATS_TRANSLUCENT) Path.Throughput = Path.Throughput * vexp(-Md.AbsorptionRate * HitTime);
+    if (MATS & (PT_MATS_TRANSLUCENT | PT_MATS_OPENPBR)) Path.Throughput = Path.Throughput * vexp(-Md.AbsorptionRate * HitTime);
 
     float ScatteringTime = PT_HIT_TIME_LIMIT;
     if ((MATS & PT_MATS_SCATTER) && Md.ScatteringRate.x > 0.0f) ScatteringTime = -pt_log(G.R01()) / Md.ScatteringRate.x;
@@ -926,6 +1137,17 @@ __global__ __launch_bounds__(256) void finalize_kernel(dscene S, uint32_t n, con
 #ifndef PT_SHADE_OTHER_MINW
 #define PT_SHADE_OTHER_MINW 5
 #endif
+// The OpenPBR instantiation (opt-in) carries the layered sampler as well: no
+// occupancy floor beyond the launch's own, so its registers are not spilled.
+#ifndef PT_SHADE_OPENPBR_MINW
+#define PT_SHADE_OPENPBR_MINW 1
+#endif
+template <uint32_t MATS>
+constexpr int ShadeMinWaves()
+{
+    return MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MINW
+         : (MATS & PT_MATS_OPENPBR) ? PT_SHADE_OPENPBR_MINW : PT_SHADE_OTHER_MINW;
+}
 // One tile of shade (basic_scatter.glsl:main for the tile's 256 slots).
 template <uint32_t MATS>
 PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const dparams& Pm, uint32_t tile)
@@ -1017,7 +1239,7 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
 }
 
 template <uint32_t MATS>
-__global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MINW : PT_SHADE_OTHER_MINW) void shade_kernel(dscene S, dslots L, dframe F,
+__global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void shade_kernel(dscene S, dslots L, dframe F,
                                                                                     dparams Pm)
 {
     // Tiles in extend's longest-first order too: tiles with long traversals
@@ -1032,7 +1254,7 @@ __global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MIN
 // of after them, and one launch replaces two.  Same per-tile work and order
 // as extend_kernel then shade_kernel, so the results are identical.
 template <uint32_t MATS, int CAP, class E>
-__global__ __launch_bounds__(256, MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MINW : PT_SHADE_OTHER_MINW) void round_kernel(
+__global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void round_kernel(
     dscene S, dslots L, dframe F, dparams Pm)
 {
     __shared__ E smem[CAP * 256];
@@ -1240,16 +1462,20 @@ static const void* RoundKernelFor(uint32_t mats, bool stack16)
     case PT_MATS_DIFFUSE | PT_MATS_METAL:
         return stack16 ? RoundKernel<PT_MATS_DIFFUSE | PT_MATS_METAL, uint16_t>()
                        : RoundKernel<PT_MATS_DIFFUSE | PT_MATS_METAL, uint32_t>();
-    default: return stack16 ? RoundKernel<PT_MATS_ALL, uint16_t>() : RoundKernel<PT_MATS_ALL, uint32_t>();
+    case PT_MATS_ALL: return stack16 ? RoundKernel<PT_MATS_ALL, uint16_t>() : RoundKernel<PT_MATS_ALL, uint32_t>();
+    default:
+        return stack16 ? RoundKernel<PT_MATS_ALL | PT_MATS_OPENPBR, uint16_t>()
+                       : RoundKernel<PT_MATS_ALL | PT_MATS_OPENPBR, uint32_t>();
     }
 }
 
 uint32_t pt_round_capacity(uint32_t scene_mats, bool stack16, uint32_t cu_count)
 {
     if (pt_extend_variant() != 0) return 0;   // round_kernel has the default variant's 20-entry stack
-    static int per_cu[3][2] = {{-1, -1}, {-1, -1}, {-1, -1}};   // by shade mask, stack entry width
+    static int per_cu[4][2] = {{-1, -1}, {-1, -1}, {-1, -1}, {-1, -1}};   // by shade mask, stack entry width
     uint32_t m = pt_shade_mats(scene_mats);
-    int& c = per_cu[m == PT_MATS_DIFFUSE ? 0 : m == (PT_MATS_DIFFUSE | PT_MATS_METAL) ? 1 : 2][stack16 ? 1 : 0];
+    int& c = per_cu[m == PT_MATS_DIFFUSE ? 0 : m == (PT_MATS_DIFFUSE | PT_MATS_METAL) ? 1 : m == PT_MATS_ALL ? 2 : 3]
+                   [stack16 ? 1 : 0];
     if (c < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&c, RoundKernelFor(scene_mats, stack16), 256, 0) != hipSuccess)
         c = 0;
     return (uint32_t)c * cu_count;
@@ -1272,7 +1498,8 @@ uint32_t pt_shade_mats(uint32_t scene_mats)
 {
     if ((scene_mats & ~(uint32_t)PT_MATS_DIFFUSE) == 0) return PT_MATS_DIFFUSE;
     if ((scene_mats & ~(uint32_t)(PT_MATS_DIFFUSE | PT_MATS_METAL)) == 0) return PT_MATS_DIFFUSE | PT_MATS_METAL;
-    return PT_MATS_ALL;
+    if (!(scene_mats & PT_MATS_OPENPBR)) return PT_MATS_ALL;
+    return PT_MATS_ALL | PT_MATS_OPENPBR;
 }
 
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
@@ -1287,8 +1514,12 @@ hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd
         hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_DIFFUSE | PT_MATS_METAL>), dim3(L.tile_count), dim3(256), 0, st,
                            S, L, F, P);
         break;
-    default:
+    case PT_MATS_ALL:
         hipLaunchKernelGGL(ptd::shade_kernel<PT_MATS_ALL>, dim3(L.tile_count), dim3(256), 0, st, S, L, F, P);
+        break;
+    default:
+        hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_ALL | PT_MATS_OPENPBR>), dim3(L.tile_count), dim3(256), 0, st,
+                           S, L, F, P);
         break;
     }
     return hipGetLastError();

@@ -76,6 +76,7 @@ enum : uint32_t {
     PT_MATS_TRANSLUCENT = 4,
     PT_MATS_SCATTER = 8,
     PT_MATS_ALL = 15,
+    PT_MATS_OPENPBR = 16,     // OpenPBR shapes shaded (ptSetBasicRendererOpenPBR); instantiated as ALL | OPENPBR
 };
 uint32_t pt_shade_mats(uint32_t scene_mats);
 hipError_t pt_launch_preview(const ptd::dscene& S, const pt_preview_parameters* p, uint32_t* spill, float4* out,

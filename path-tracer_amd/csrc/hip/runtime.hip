@@ -161,6 +161,7 @@ struct pt_basic_renderer {
     static constexpr uint32_t MAX_GROUPS = 4;
     uint32_t groups = 1;
     int fused = FusedDefault();         // fused rounds mode (ptSetBasicRendererFusedRounds)
+    int openpbr = 0;                    // shade OpenPBR materials (ptSetBasicRendererOpenPBR)
     hipStream_t gstream[MAX_GROUPS] = {};
     hipEvent_t gevent[MAX_GROUPS] = {};
     hipEvent_t fork = nullptr;
@@ -515,6 +516,7 @@ static uint32_t SceneMaterialMask(const pt_scene_packs* p)
         if (type == PT_MATERIAL_TYPE_BASIC_DIFFUSE) m |= PT_MATS_DIFFUSE;
         else if (type == PT_MATERIAL_TYPE_BASIC_METAL) m |= PT_MATS_METAL;
         else if (type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT) m |= PT_MATS_TRANSLUCENT;
+        else if (type == PT_MATERIAL_TYPE_OPENPBR) m |= PT_MATS_OPENPBR;
     }
     if ((m & PT_MATS_TRANSLUCENT) || p->globals->SceneScatterRate > 0.0f) m |= PT_MATS_SCATTER;
     return m;
@@ -585,7 +587,7 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     D.atlas_tiled = s->atlas_tiled ? 1u : 0u;
     D.fast_div = FastDivBoxes(p) ? 1u : 0u;
     s->mats = SceneMaterialMask(p);
-    uint32_t types = s->mats & (PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_TRANSLUCENT);
+    uint32_t types = s->mats & (PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_TRANSLUCENT | PT_MATS_OPENPBR);
     D.mat_classes = (types & (types - 1)) != 0 ? 1u : 0u;   // more than one material type
     D.blas_words = BlasWordsPackable(p) ? 1u : 0u;
     D.blas_firstbits = 0;
@@ -851,11 +853,23 @@ int ptResetBasicRenderer(pt_device* d, pt_basic_renderer* r)
 // at once -- a rank's share of a strongly scaled frame -- and the scene needs
 // no spilled stack (renderer mode 1); mode 0 never fuses, mode 2 fuses
 // whenever the kernel applies (tests and A/B).
+// Material mask the renderer shades with (shade / round instantiation): the
+// scene's OpenPBR shapes, and the media they bring, join it only when OpenPBR
+// shading is enabled (ptSetBasicRendererOpenPBR); otherwise their hits end
+// the path as in the reference.
+static uint32_t ShadeMats(const pt_basic_renderer* r)
+{
+    uint32_t m = r->scene->mats;
+    if (!(m & PT_MATS_OPENPBR)) return m;
+    if (!r->openpbr) return m & ~(uint32_t)PT_MATS_OPENPBR;
+    return m | PT_MATS_SCATTER;
+}
+
 static bool RoundFused(const pt_basic_renderer* r, const ptd::dslots& g)
 {
     const int mode = r->fused;
     if (mode == 0 || g.spill || g.tile_count == 0) return false;
-    uint32_t cap = pt_round_capacity(r->scene->mats, r->scene->d.stack16 != 0, r->dev->cu_count);
+    uint32_t cap = pt_round_capacity(ShadeMats(r), r->scene->d.stack16 != 0, r->dev->cu_count);
     if (cap == 0) return false;
     return mode == 2 || g.tile_count <= cap;
 }
@@ -895,7 +909,7 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
             event_pair ep{};
             if (RoundFused(r, gs[g])) {
                 if (int e = BeginTimed(d, PT_KERNEL_ROUND, ep, sampled, st[g])) return e;
-                PT_HIP(pt_launch_round(r->scene->d, gs[g], F, P, r->scene->mats, st[g]));
+                PT_HIP(pt_launch_round(r->scene->d, gs[g], F, P, ShadeMats(r), st[g]));
                 if (int e = EndTimed(d, ep)) return e;
                 if (sort) PT_HIP(pt_launch_tile_order(gs[g], st[g]));
                 continue;
@@ -904,7 +918,7 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
             PT_HIP(pt_launch_extend(r->scene->d, gs[g], F, r->slots.spill, st[g]));
             if (int e = EndTimed(d, ep)) return e;
             if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled, st[g])) return e;
-            PT_HIP(pt_launch_shade(r->scene->d, gs[g], F, P, r->scene->mats, st[g]));
+            PT_HIP(pt_launch_shade(r->scene->d, gs[g], F, P, ShadeMats(r), st[g]));
             if (int e = EndTimed(d, ep)) return e;
             if (sort) PT_HIP(pt_launch_tile_order(gs[g], st[g]));
         }
@@ -924,6 +938,13 @@ int ptSetBasicRendererFusedRounds(pt_basic_renderer* r, int mode)
 {
     if (!r || mode < 0 || mode > 2) { SetError("ptSetBasicRendererFusedRounds: bad argument"); return -1; }
     r->fused = mode;
+    return 0;
+}
+
+int ptSetBasicRendererOpenPBR(pt_basic_renderer* r, int enable)
+{
+    if (!r || enable < 0 || enable > 1) { SetError("ptSetBasicRendererOpenPBR: bad argument"); return -1; }
+    r->openpbr = enable;
     return 0;
 }
 

@@ -135,6 +135,29 @@ int ptsSetMaterialParameter(pts_scene* s, pts_material* mp, const char* name, co
     else if (k == "AbbeNumber") rc = flt(m->AbbeNumber);
     else if (k == "TransmissionDepth") rc = flt(m->TransmissionDepth);
     else if (k == "ScatteringAnisotropy") rc = flt(m->ScatteringAnisotropy);
+    // OpenPBR (openpbr.hpp:5-37); its SpecularRoughness is "Roughness" above
+    else if (k == "BaseWeight") rc = flt(m->BaseWeight);
+    else if (k == "BaseMetalness") rc = flt(m->BaseMetalness);
+    else if (k == "BaseDiffuseRoughness") rc = flt(m->BaseDiffuseRoughness);
+    else if (k == "SpecularWeight") rc = flt(m->SpecularWeight);
+    else if (k == "SpecularIOR") rc = flt(m->SpecularIOR);
+    else if (k == "TransmissionWeight") rc = flt(m->TransmissionWeight);
+    else if (k == "TransmissionScatter") rc = vec(m->TransmissionScatter);
+    else if (k == "TransmissionScatterAnisotropy") rc = flt(m->TransmissionScatterAnisotropy);
+    else if (k == "TransmissionDispersionScale") rc = flt(m->TransmissionDispersionScale);
+    else if (k == "TransmissionDispersionAbbeNumber") rc = flt(m->TransmissionDispersionAbbeNumber);
+    else if (k == "CoatWeight") rc = flt(m->CoatWeight);
+    else if (k == "CoatColor") rc = vec(m->CoatColor);
+    else if (k == "CoatRoughness") rc = flt(m->CoatRoughness);
+    else if (k == "CoatRoughnessAnisotropy") rc = flt(m->CoatRoughnessAnisotropy);
+    else if (k == "CoatIOR") rc = flt(m->CoatIOR);
+    else if (k == "CoatDarkening") rc = flt(m->CoatDarkening);
+    else if (k == "EmissionLuminance") rc = flt(m->EmissionLuminance);
+    else if (k == "EmissionColor") rc = vec(m->EmissionColor);
+    else if (k == "LayerBounceLimit") {
+        rc = n == 1 && v[0] >= 0.0f && v[0] <= 1024.0f && v[0] == (float)(int)v[0] ? 0 : -1;
+        if (rc == 0) m->LayerBounceLimit = (int)v[0];
+    }
     else { g_err = "unknown material parameter " + k; return -1; }
     if (rc) { g_err = "wrong value count for " + k; return -1; }
     S(s)->DirtyFlags |= PT_SCENE_DIRTY_MATERIALS;
@@ -150,6 +173,7 @@ int ptsSetMaterialTexture(pts_scene* s, pts_material* mp, const char* name, pts_
     else if (k == "SpecularTexture") m->SpecularTexture = tx;
     else if (k == "RoughnessTexture") m->RoughnessTexture = tx;
     else if (k == "RoughnessAnisotropyTexture") m->RoughnessAnisotropyTexture = tx;
+    else if (k == "EmissionColorTexture") m->EmissionColorTexture = tx;
     else { g_err = "unknown material texture " + k; return -1; }
     S(s)->DirtyFlags |= PT_SCENE_DIRTY_MATERIALS;
     return 0;

@@ -417,34 +417,35 @@ static void PackMaterialData(scene* Scene, material* M, uint32_t* A)
             Spec(M->ScatteringColor, &A[PT_BASIC_TRANSLUCENT_SCATTERING_SPECTRUM]);
             A[PT_BASIC_TRANSLUCENT_SCATTERING_ANISOTROPY] = F2U(M->ScatteringAnisotropy);
             break;
-        case PT_MATERIAL_TYPE_OPENPBR: {           // openpbr.hpp:52-134 (packed, never shaded)
-            A[1] = static_cast<uint32_t>(M->LayerBounceLimit);
-            A[2] = F2U(M->BaseWeight);
-            Spec(M->BaseColor, &A[3]);
-            A[6] = GetPackedTextureIndex(M->BaseTexture);
-            A[7] = F2U(M->BaseMetalness);
-            A[8] = F2U(M->BaseDiffuseRoughness);
-            A[9] = F2U(M->SpecularWeight);
-            Spec(M->SpecularColor, &A[10]);
-            A[13] = F2U(M->SpecularIOR);
-            A[14] = F2U(M->Roughness);
-            A[15] = GetPackedTextureIndex(M->RoughnessTexture);
-            A[16] = F2U(M->RoughnessAnisotropy);
-            Spec(M->TransmissionColor, &A[17]);
-            A[20] = F2U(M->TransmissionWeight);
-            Spec(M->TransmissionScatter, &A[21]);
-            A[24] = F2U(M->TransmissionScatterAnisotropy);
-            A[25] = F2U(M->TransmissionDepth);
-            A[26] = F2U(M->TransmissionDispersionAbbeNumber / M->TransmissionDispersionScale);
-            Spec(M->EmissionColor, &A[27]);
-            A[30] = GetPackedTextureIndex(M->EmissionColorTexture);
-            A[31] = F2U(M->EmissionLuminance);
-            A[32] = F2U(M->CoatWeight);
-            Spec(M->CoatColor, &A[33]);
-            A[36] = F2U(M->CoatIOR);
-            A[37] = F2U(M->CoatRoughness);
-            A[38] = F2U(M->CoatRoughnessAnisotropy);
-            A[39] = F2U(M->CoatDarkening);
+        case PT_MATERIAL_TYPE_OPENPBR: {           // openpbr.hpp:52-134
+            A[PT_OPENPBR_LAYER_BOUNCE_LIMIT] = static_cast<uint32_t>(M->LayerBounceLimit);
+            A[PT_OPENPBR_BASE_WEIGHT] = F2U(M->BaseWeight);
+            Spec(M->BaseColor, &A[PT_OPENPBR_BASE_SPECTRUM]);
+            A[PT_OPENPBR_BASE_SPECTRUM_TEXTURE_INDEX] = GetPackedTextureIndex(M->BaseTexture);
+            A[PT_OPENPBR_BASE_METALNESS] = F2U(M->BaseMetalness);
+            A[PT_OPENPBR_BASE_DIFFUSE_ROUGHNESS] = F2U(M->BaseDiffuseRoughness);
+            A[PT_OPENPBR_SPECULAR_WEIGHT] = F2U(M->SpecularWeight);
+            Spec(M->SpecularColor, &A[PT_OPENPBR_SPECULAR_SPECTRUM]);
+            A[PT_OPENPBR_SPECULAR_IOR] = F2U(M->SpecularIOR);
+            A[PT_OPENPBR_SPECULAR_ROUGHNESS] = F2U(M->Roughness);
+            A[PT_OPENPBR_SPECULAR_ROUGHNESS_TEXTURE_INDEX] = GetPackedTextureIndex(M->RoughnessTexture);
+            A[PT_OPENPBR_SPECULAR_ROUGHNESS_ANISOTROPY] = F2U(M->RoughnessAnisotropy);
+            Spec(M->TransmissionColor, &A[PT_OPENPBR_TRANSMISSION_SPECTRUM]);
+            A[PT_OPENPBR_TRANSMISSION_WEIGHT] = F2U(M->TransmissionWeight);
+            Spec(M->TransmissionScatter, &A[PT_OPENPBR_TRANSMISSION_SCATTER_SPECTRUM]);
+            A[PT_OPENPBR_TRANSMISSION_SCATTER_ANISOTROPY] = F2U(M->TransmissionScatterAnisotropy);
+            A[PT_OPENPBR_TRANSMISSION_DEPTH] = F2U(M->TransmissionDepth);
+            A[PT_OPENPBR_TRANSMISSION_DISPERSION_ABBE_NUMBER] =
+                F2U(M->TransmissionDispersionAbbeNumber / M->TransmissionDispersionScale);
+            Spec(M->EmissionColor, &A[PT_OPENPBR_EMISSION_SPECTRUM]);
+            A[PT_OPENPBR_EMISSION_SPECTRUM_TEXTURE_INDEX] = GetPackedTextureIndex(M->EmissionColorTexture);
+            A[PT_OPENPBR_EMISSION_LUMINANCE] = F2U(M->EmissionLuminance);
+            A[PT_OPENPBR_COAT_WEIGHT] = F2U(M->CoatWeight);
+            Spec(M->CoatColor, &A[PT_OPENPBR_COAT_COLOR_SPECTRUM]);
+            A[PT_OPENPBR_COAT_IOR] = F2U(M->CoatIOR);
+            A[PT_OPENPBR_COAT_ROUGHNESS] = F2U(M->CoatRoughness);
+            A[PT_OPENPBR_COAT_ROUGHNESS_ANISOTROPY] = F2U(M->CoatRoughnessAnisotropy);
+            A[PT_OPENPBR_COAT_DARKENING] = F2U(M->CoatDarkening);
             break;
         }
     }

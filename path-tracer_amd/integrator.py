@@ -228,6 +228,11 @@ class BasicRenderer:
         """0 never / 1 automatic / 2 whenever possible (ptSetBasicRendererFusedRounds)."""
         _check(N.hip_lib().ptSetBasicRendererFusedRounds(self._h, int(mode)), "ptSetBasicRendererFusedRounds")
 
+    def set_openpbr(self, enable: bool):
+        """Shade OpenPBR materials (ptSetBasicRendererOpenPBR); off by default,
+        as in the reference, where an OpenPBR hit ends the path."""
+        _check(N.hip_lib().ptSetBasicRendererOpenPBR(self._h, int(bool(enable))), "ptSetBasicRendererOpenPBR")
+
     def reset(self):
         _check(N.hip_lib().ptResetBasicRenderer(self.device.handle, self._h), "ptResetBasicRenderer")
 

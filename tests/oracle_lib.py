@@ -33,6 +33,7 @@ def lib():
         L.oracle_destroy.argtypes = [vp]
         L.oracle_params.restype = vp
         L.oracle_params.argtypes = [vp]
+        L.oracle_set_openpbr.argtypes = [vp, C.c_int]
         L.oracle_reset.argtypes = [vp]
         L.oracle_run.argtypes = [vp, u32]
         L.oracle_read_accum.argtypes = [vp, fptr]
@@ -79,6 +80,10 @@ class OracleRenderer:
             setattr(self._params.contents, name, value)
         else:
             object.__setattr__(self, name, value)
+
+    def set_openpbr(self, enable):
+        """OpenPBR shading on/off (ptSetBasicRendererOpenPBR's counterpart)."""
+        lib().oracle_set_openpbr(self._h, int(bool(enable)))
 
     def reset(self):
         lib().oracle_reset(self._h)
