@@ -943,6 +943,12 @@ PT_DEV void ExtendRay(const dscene& S, const Src& src, tstack<SPILL, CAP, E>& st
                     else if (u == 96) __builtin_amdgcn_s_setprio(3);
                 }
             }
+#elif PT_EXP_STEP_CAP
+            // Experiment only (not bit-exact): traversal cut after
+            // PT_EXP_STEP_CAP steps, to measure what the longest rays cost.
+            uint32_t it = 0;
+            while (!LaneStep<SPILL, CAP, Src, no_stats, true, E>(S, Ln, st, src, slot, ns) && ++it < PT_EXP_STEP_CAP) {}
+            if (Ln.Shape == 0xFFFFFFFEu) Ln.Shape = Ln.blas;   // cut inside a BLAS: its instance
 #else
             while (!LaneStep<SPILL, CAP, Src, no_stats, true, E>(S, Ln, st, src, slot, ns)) {}
 #endif
