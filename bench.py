@@ -5,10 +5,19 @@
 A step is one integrator round (extend + shade over every pixel slot, i.e.
 one RunBasicRenderer(1)).  Inputs (scene, slot state) are resident in HBM
 before timing starts.  For N GPUs (one process per GPU, launched by
-torch.distributed.run) the config's frame is split into 16-row bands, band b
-on rank b % N (strong scaling: the frame is fixed, each rank traces 1/N of
-it); the frame-end exchange (RCCL point-to-point gather of every rank's
-bands to rank 0, ptCommGatherSampleBuffer) is inside the timed region.
+torch.distributed.run) the job is sharded one of two ways (--shard):
+
+* samples (default, all single-GPU configs): north_star's "pixels/samples
+  shard embarrassingly ... RCCL reduce of the per-pixel radiance and
+  sample-count buffers at frame end".  Every rank renders the whole frame with
+  its own RNG stream (FrameIndex offset rank << 24), so the frame's spp
+  target is split over the ranks; the frame-end ncclReduce of the XYZ sums and
+  sample counts into rank 0's total buffer (ptCommReduceSampleBufferInto) is
+  inside the timed region.  Per-GPU work per step is fixed: "weak".
+* bands (default for C4, "pixel-tiled across 8xMI355X"): the frame is split
+  into 16-row bands, band b on rank b % N (strong scaling: each rank traces
+  1/N of the frame); the frame-end RCCL point-to-point gather of every rank's
+  bands to rank 0 (ptCommGatherSampleBuffer) is inside the timed region.
 
 Prints ONE JSON line on rank 0.
 """
@@ -138,7 +147,13 @@ def main():
     ap.add_argument("--profile-period", type=int, default=4,
                     help="time the kernels of every N-th step (HIP events) inside the timed loop")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--one-gpu-flow-check", action="store_true",
+                    help="every rank on device 0 (multi-rank flow check on a one-GPU box; timings not meaningful)")
+    ap.add_argument("--shard", choices=("auto", "samples", "bands"), default="auto",
+                    help="multi-GPU split: samples (whole frame per rank, own RNG stream) or 16-row pixel bands; "
+                         "auto = bands for C4 (pixel-tiled by its config), samples otherwise")
     args = ap.parse_args()
+    shard = args.shard if args.shard != "auto" else ("bands" if args.config == 4 else "samples")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -154,20 +169,59 @@ def main():
     info = scene.info
     width, height = info.width, info.height
 
-    dev = pt.Device(local_rank)
+    dev = pt.Device(0 if args.one_gpu_flow_check else local_rank)
     dscene = pt.DeviceScene(dev)
     dscene.update(scene)
     sb = pt.SampleBuffer(dev, width, height)
-    r = pt.BasicRenderer(dev, dscene, sb, rank=rank, nranks=world)
+    part_rank, part_n = (rank, world) if shard == "bands" else (0, 1)
+    r = pt.BasicRenderer(dev, dscene, sb, rank=part_rank, nranks=part_n)
     r.RenderFlags = info.render_flags
     r.PathTerminationProbability = info.termination_probability
+    # Sample shards: rank r's RNG stream starts at FrameIndex r << 24 (seeds
+    # are hashed from (x, y, FrameIndex), scene.glsl.inc / basic.cpp:285-332).
+    if shard == "samples":
+        r.FrameIndex = rank << 24
+    total = pt.SampleBuffer(dev, width, height) if (world > 1 and shard == "samples" and rank == 0) else None
     comm = None
+    exchange = None
     if world > 1:
         import torch
         uid = bytearray(pt.Comm.unique_id()) if rank == 0 else bytearray(128)
         t = torch.tensor(list(uid), dtype=torch.uint8)
         dist.broadcast(t, 0)
-        comm = pt.Comm(dev, world, rank, bytes(t.tolist()))
+        # RCCL over xGMI; if the communicator cannot be built (e.g. two ranks
+        # on one device, which RCCL refuses) the frame-end exchange falls back
+        # to a gloo reduce through host memory, and the line says so.
+        try:
+            comm = pt.Comm(dev, world, rank, bytes(t.tolist()))
+            exchange = "rccl"
+        except Exception as e:   # noqa: BLE001
+            print(f"bench: RCCL communicator unavailable ({e}); gloo fallback", file=sys.stderr, flush=True)
+            exchange = "gloo-fallback"
+        ok = torch.tensor([1 if comm is not None else 0], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0 and comm is not None:   # every rank takes the same path
+            comm.close()
+            comm, exchange = None, "gloo-fallback"
+
+    def frame_end_exchange():
+        """The frame-end exchange (inside the timed region)."""
+        if world == 1:
+            return
+        if comm is not None:
+            if shard == "samples":
+                comm.reduce_sample_buffer_into(sb, total, 0)
+            else:
+                comm.gather_sample_buffer(sb, 0)
+            return
+        import torch
+        a = sb.read()
+        if shard == "bands":
+            a[~pt.owned_pixels(width, height, rank, world)] = 0.0
+        acc = torch.from_numpy(a)
+        dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
+        if rank == 0:
+            (total if shard == "samples" else sb).write(acc.numpy())
 
     # Reset + Run(2) as after a restart (application.cpp:109-110), then the
     # path population settles (the first ~30 rounds after a restart run ~4 %
@@ -195,8 +249,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         r.run(1)
-    if comm is not None:
-        comm.gather_sample_buffer(sb, 0)
+    frame_end_exchange()
     dev.synchronize()
     barrier()
     dt = time.perf_counter() - t0
@@ -208,7 +261,7 @@ def main():
     # Traversal counters of one extra extend over the current rays (outside
     # the timed region; the next Run overwrites the same hit records).
     trav = r.extend_stats()
-    slots_owned = int(np.sum(pt.owned_pixels(width, height, rank, world)))
+    slots_owned = int(np.sum(pt.owned_pixels(width, height, part_rank, part_n)))
     # Rays traced and paths completed in the timed steps (ptGetStats; the
     # sample count equals the accumulator's alpha increments).
     rays1, samples1 = r.stats()
@@ -226,7 +279,7 @@ def main():
         rays, samples = float(rays_local), float(samples_local)
 
     def shutdown():
-        for x in (r, sb, dscene):
+        for x in (r, sb, dscene) + ((total,) if total is not None else ()):
             x.close()
         if comm is not None:
             comm.close()
@@ -248,6 +301,7 @@ def main():
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
     achieved = kernels[dom]["gbps"]
     traffic, traffic_src = measured_traffic(dom)
+    xname = "RCCL" if exchange == "rccl" else "gloo (host-memory fallback)"
     metric = ("Mrays/s + Msamples/s, Viking Room 1920x1080 1024spp, 1/2/4/8 GPUs" if args.config == 3 else
               f"Mrays/s + Msamples/s, C{args.config} {info.width}x{info.height} {info.spp}spp")
     out = {
@@ -259,18 +313,27 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak" if (shard == "samples" and world > 1) else "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": f"synthetic (procedural {info.mesh_face_count}-triangle room mesh + 1024^2 texture; "
                 "Viking Room asset absent)",
         "config": {
-            "workload": f"C{args.config} scene, {width}x{height} px frame split in 16-row bands over {world} GPU(s) "
-                        f"({slots_owned} px on rank 0), one round (extend+shade of every pixel's path) per step",
+            "workload": (f"C{args.config} scene, {width}x{height} px frame split in 16-row bands over {world} GPU(s) "
+                         f"({slots_owned} px on rank 0), one round (extend+shade of every pixel's path) per step"
+                         if shard == "bands" else
+                         f"C{args.config} scene, {width}x{height} px frame; each of {world} GPU(s) renders every pixel "
+                         f"with its own RNG stream (the spp target split over the GPUs), one round (extend+shade of "
+                         f"every pixel's path) per step per GPU"),
+            "shard": shard,
+            "exchange": exchange,
             "spp_target": info.spp,
             "settle_rounds": SETTLE_ROUNDS,
             "mesh_faces": info.mesh_face_count,
-            "parallelism": f"pixel-bands x{world}" + (" + RCCL band gather to rank 0" if world > 1 else ""),
+            "parallelism": (f"pixel-bands x{world}" + (f" + {xname} band gather to rank 0" if world > 1 else "")
+                            if shard == "bands" else
+                            f"sample-shards x{world}" + (f" + {xname} reduce of radiance + sample counts to rank 0"
+                                                         if world > 1 else "")),
         },
         "msamples_per_s": round(samples / dt / 1e6, 3),
         "roofline": {

@@ -280,6 +280,17 @@ int      ptCommReduceSampleBuffer(pt_device* device, pt_comm* comm, pt_sample_bu
  * the call the root's buffer holds every rank's bands; other ranks' buffers
  * are unchanged.  Repeatable after further rounds. */
 int      ptCommGatherSampleBuffer(pt_device* device, pt_comm* comm, pt_sample_buffer* buffer, int root);
+/* Sample sharding (north_star: "pixels/samples shard ... RCCL reduce of the
+ * per-pixel radiance and sample-count buffers at frame end"): every rank
+ * renders the whole frame with its own RNG stream (a FrameIndex offset per
+ * rank) and keeps its own running accumulator; this out-of-place
+ * ncclReduce(sum) leaves in `total` on `root` the sum over ranks of their
+ * XYZ radiance sums and sample counts, which the resolve averages.  The
+ * ranks' own accumulators are unchanged, so the call may repeat after more
+ * rounds (progressive frames).  `total` is read only on `root` (may be NULL
+ * elsewhere) and must match `buffer`'s size. */
+int      ptCommReduceSampleBufferInto(pt_device* device, pt_comm* comm, pt_sample_buffer* buffer,
+                                      pt_sample_buffer* total, int root);
 
 #ifdef __cplusplus
 }

@@ -258,6 +258,7 @@ HIP_API = {
     "ptCommDestroy": (None, [_vp]),
     "ptCommReduceSampleBuffer": (_i32, [_vp, _vp, _vp, _i32]),
     "ptCommGatherSampleBuffer": (_i32, [_vp, _vp, _vp, _i32]),
+    "ptCommReduceSampleBufferInto": (_i32, [_vp, _vp, _vp, _vp, _i32]),
 }
 
 _scene_lib = None

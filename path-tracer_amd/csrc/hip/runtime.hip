@@ -1321,6 +1321,23 @@ int ptCommReduceSampleBuffer(pt_device* d, pt_comm* c, pt_sample_buffer* b, int 
     return 0;
 }
 
+int ptCommReduceSampleBufferInto(pt_device* d, pt_comm* c, pt_sample_buffer* b, pt_sample_buffer* total, int root)
+{
+    if (!d || !c || !b) { SetError("null argument"); return -1; }
+    if (root < 0 || root >= c->nranks) { SetError("bad root %d", root); return -1; }
+    const bool is_root = c->rank == root;
+    if (is_root && (!total || total->width != b->width || total->height != b->height)) {
+        SetError("ptCommReduceSampleBufferInto: the root needs a total buffer of the same size");
+        return -1;
+    }
+    PT_HIP(hipSetDevice(d->id));
+    size_t count = (size_t)b->width * b->height * 4;
+    ncclResult_t e = ncclReduce(b->accum, is_root ? total->accum : b->accum, count, ncclFloat32, ncclSum, root, c->comm,
+                                d->stream);
+    if (e != ncclSuccess) { SetError("ncclReduce: %s", ncclGetErrorString(e)); return (int)e; }
+    return 0;
+}
+
 // The same frame-end exchange with 1/N of the traffic: the bands are
 // disjoint, so the root needs only each band's owner's rows.  Band b (rows
 // [16b, 16b+16), contiguous in the row-major buffer) is owned by rank

@@ -363,6 +363,14 @@ class Comm:
         _check(N.hip_lib().ptCommReduceSampleBuffer(self.device.handle, self._h, sample_buffer.handle, root),
                "ptCommReduceSampleBuffer")
 
+    def reduce_sample_buffer_into(self, sample_buffer: SampleBuffer, total: SampleBuffer | None, root: int = 0):
+        """Sample sharding: `total` on `root` = sum over ranks of their own
+        accumulators (ptCommReduceSampleBufferInto); `total` may be None
+        on the other ranks."""
+        _check(N.hip_lib().ptCommReduceSampleBufferInto(self.device.handle, self._h, sample_buffer.handle,
+                                                         total.handle if total is not None else None, root),
+               "ptCommReduceSampleBufferInto")
+
     def gather_sample_buffer(self, sample_buffer: SampleBuffer, root: int = 0):
         """Each rank's own bands, point-to-point to `root` (1/N of the reduce's traffic)."""
         _check(N.hip_lib().ptCommGatherSampleBuffer(self.device.handle, self._h, sample_buffer.handle, root),

@@ -10,6 +10,9 @@ the max-over-ranks wall time.
 
 PT_DIST_RENDERER=gpu renders with the product (libpathtracer.so, every rank
 on device 0, -m gpu tests); the default is the CPU oracle (the CPU suite).
+PT_DIST_SHARD=samples: sample sharding instead (bench.py's default) -- every
+rank renders the whole frame from FrameIndex rank << 24 and the whole
+accumulators are summed (the stand-in for ptCommReduceSampleBufferInto).
 """
 from __future__ import annotations
 
@@ -35,18 +38,22 @@ def main():
     pt = conftest.load_package()
     scene = pt.Scene.config(cfg)
     gpu = os.environ.get("PT_DIST_RENDERER") == "gpu"
+    samples = os.environ.get("PT_DIST_SHARD") == "samples"
+    prank, pn = (0, 1) if samples else (rank, world)
     if gpu:
         dev = pt.Device(0)
         ds = pt.DeviceScene(dev)
         ds.update(scene)
         sb = pt.SampleBuffer(dev, W, H)
-        r = pt.BasicRenderer(dev, ds, sb, rank=rank, nranks=world)
+        r = pt.BasicRenderer(dev, ds, sb, rank=prank, nranks=pn)
         accum = sb.read
     else:
-        r = oracle_lib.OracleRenderer(scene.packs(), W, H, rank=rank, nranks=world, threads=2)
+        r = oracle_lib.OracleRenderer(scene.packs(), W, H, rank=prank, nranks=pn, threads=2)
         accum = r.accum
     r.RenderFlags = 3
-    owned = pt.owned_pixels(W, H, rank, world)
+    if samples:
+        r.FrameIndex = rank << 24
+    owned = pt.owned_pixels(W, H, prank, pn)
     frames = []
     dist.barrier()
     t0 = time.perf_counter()

@@ -52,6 +52,39 @@ def test_two_rank_band_render_reduces_to_full_frame(pt, tmp_path):
     assert np.array_equal(got["accum2"].view(np.uint32), full2.view(np.uint32))
 
 
+def test_two_rank_sample_shards_reduce_to_sum(pt, tmp_path):
+    """Sample sharding (bench.py's default): both ranks render the whole
+    frame, rank r from FrameIndex r << 24; the reduced frames are the sum of
+    the two single-process renders with those offsets."""
+    cfg, W, H = 1, 40, 24
+    out = tmp_path / "reduced.npz"
+    env = dict(os.environ, OMP_NUM_THREADS="2", HSA_ENABLE_IPC_MODE_LEGACY="0", PT_DIST_SHARD="samples")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           str(HERE / "dist_worker.py"), str(out), str(cfg), str(W), str(H)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = np.load(out)
+    assert int(got["owned"][0]) == 2 * W * H       # every rank renders every pixel
+    s = pt.Scene.config(cfg)
+    want = [np.zeros((H, W, 4), np.float32), np.zeros((H, W, 4), np.float32)]
+    for rank in range(2):
+        o = oracle_lib.OracleRenderer(s.packs(), W, H, threads=2)
+        o.RenderFlags = 3
+        o.FrameIndex = rank << 24
+        o.reset()
+        o.run(2)
+        o.run(1)
+        want[0] = want[0] + o.accum()
+        o.run(1)
+        want[1] = want[1] + o.accum()
+        o.close()
+    s.close()
+    assert np.array_equal(got["accum"].view(np.uint32), want[0].view(np.uint32))
+    assert np.array_equal(got["accum2"].view(np.uint32), want[1].view(np.uint32))
+    assert got["accum"][..., 3].sum() > 0
+
+
 def test_band_ownership(pt):
     for H in (16, 80, 1080, 2160):
         for N in (1, 2, 3, 8):

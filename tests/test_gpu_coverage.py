@@ -306,3 +306,80 @@ def test_comm_gather_single_rank_and_partition_check(pt, dev):
     for x in (r2, r, sb, ds):
         x.close()
     s.close()
+
+
+def test_sample_shard_offset_and_reduce_into(pt, dev):
+    """Sample sharding (bench.py's default multi-GPU split): a renderer whose
+    RNG stream starts at FrameIndex 1 << 24 (rank 1's) is bit-exact against the
+    oracle from the same offset; ptCommReduceSampleBufferInto on a one-rank
+    communicator copies the accumulator into the total, leaving it intact,
+    and is repeatable after more rounds."""
+    s = pt.Scene.config(5)
+    W, H = 128, 64
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    sb = pt.SampleBuffer(dev, W, H)
+    total = pt.SampleBuffer(dev, W, H)
+    r = pt.BasicRenderer(dev, ds, sb)
+    o = oracle_lib.OracleRenderer(s.packs(), W, H)
+    comm = pt.Comm(dev, 1, 0, pt.Comm.unique_id())
+    for x in (r, o):
+        x.RenderFlags = 3
+        x.FrameIndex = 1 << 24
+        x.reset()
+        x.run(2)
+        x.run(1)
+    for frame in range(2):
+        comm.reduce_sample_buffer_into(sb, total, 0)
+        dev.synchronize()
+        compare_state(r.read_state(), o.state())
+        assert np.array_equal(bits(sb.read()), bits(o.accum()))
+        assert np.array_equal(bits(total.read()), bits(o.accum()))
+        for x in (r, o):
+            x.run(1)
+    assert r.FrameIndex == (1 << 24) + 4          # Run(2), Run(1) and two more Run(1)
+    with pytest.raises(pt.PathTracerError):
+        comm.reduce_sample_buffer_into(sb, None, 0)     # the root needs a total buffer
+    comm.close()
+    o.close()
+    for x in (r, total, sb, ds):
+        x.close()
+    s.close()
+
+
+def test_two_process_sample_shards_equal_summed_renders(pt, dev, tmp_path):
+    """Two processes on this GPU, each rendering the whole C5 frame from its
+    own FrameIndex offset with the product renderer, summed over gloo (the
+    CPU stand-in for the RCCL reduce): equal to this process's two offset
+    renders added."""
+    cfg, W, H = 5, 96, 64
+    out = tmp_path / "reduced.npz"
+    env = dict(os.environ, OMP_NUM_THREADS="2", HSA_ENABLE_IPC_MODE_LEGACY="0", PT_DIST_RENDERER="gpu",
+               PT_DIST_SHARD="samples")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           str(HERE / "dist_worker.py"), str(out), str(cfg), str(W), str(H)]
+    res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr[-3000:]
+    got = np.load(out)
+    s = pt.Scene.config(cfg)
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    want = [np.zeros((H, W, 4), np.float32), np.zeros((H, W, 4), np.float32)]
+    for rank in range(2):
+        sb = pt.SampleBuffer(dev, W, H)
+        r = pt.BasicRenderer(dev, ds, sb)
+        r.RenderFlags = 3
+        r.FrameIndex = rank << 24
+        r.reset()
+        r.run(2)
+        r.run(1)
+        want[0] = want[0] + sb.read()
+        r.run(1)
+        want[1] = want[1] + sb.read()
+        r.close()
+        sb.close()
+    assert np.array_equal(bits(got["accum"]), bits(want[0]))
+    assert np.array_equal(bits(got["accum2"]), bits(want[1]))
+    ds.close()
+    s.close()
