@@ -123,10 +123,15 @@ pt3 UnpackUnitVector(uint32_t PackedV)                                          
     return normalize(v3(P.x, P.y, Z));
 }
 
+// The division (Min - Ray.Origin) / Ray.Velocity is evaluated as
+// RN((Min - Ray.Origin) * RN(1 / Ray.Velocity)): GLSL allows `/` 2.5 ULP and
+// GPU compilers emit this reciprocal form for it (numerics convention,
+// DESIGN.md §2); the HIP slab test evaluates the same expression.
 float IntersectBoundingBox(const ray& Ray, float Reach, pt3 Min, pt3 Max)                            // :153-185
 {
-    pt3 MinT = (Min - Ray.Origin) / Ray.Velocity;
-    pt3 MaxT = (Max - Ray.Origin) / Ray.Velocity;
+    pt3 InverseVelocity = v3(1.0f / Ray.Velocity.x, 1.0f / Ray.Velocity.y, 1.0f / Ray.Velocity.z);
+    pt3 MinT = (Min - Ray.Origin) * InverseVelocity;
+    pt3 MaxT = (Max - Ray.Origin) * InverseVelocity;
     pt3 EarlierT = vmin(MinT, MaxT);
     pt3 LaterT = vmax(MinT, MaxT);
     float EntryT = pt_max(pt_max(EarlierT.x, EarlierT.y), EarlierT.z);

@@ -442,24 +442,6 @@ void ptDestroyScene(pt_device* d, pt_scene* s)
 }
 
 // UpdateVulkanScene (scene.cpp:1692-2006): synchronous upload of the packs.
-// Box-coordinate condition of the extend kernel's exact fast slab division
-// (pt_device.hpp, IntersectBoundingBox): every TLAS / BLAS bound is 0 or has
-// magnitude in [2^-50, 2^40].  Scenes outside it trace with IEEE division.
-static bool FastDivBoxes(const pt_scene_packs* p)
-{
-    auto ok = [](float c) {
-        float m = std::fabs(c);
-        return m == 0.0f || (m >= 0x1p-50f && m <= 0x1p40f);
-    };
-    for (uint32_t i = 0; i < p->shape_node_count; i++)
-        for (int k = 0; k < 3; k++)
-            if (!ok(p->shape_nodes[i].Minimum[k]) || !ok(p->shape_nodes[i].Maximum[k])) return false;
-    for (uint32_t i = 0; i < p->mesh_node_count; i++)
-        for (int k = 0; k < 3; k++)
-            if (!ok(p->mesh_nodes[i].Minimum[k]) || !ok(p->mesh_nodes[i].Maximum[k])) return false;
-    return true;
-}
-
 // Whether every BLAS node's index words fit one packed stack entry
 // (PackBlasEntry): leaves with <= 31 faces starting below 2^26, child-pair
 // indices below 2^31.  PT_BLAS_WORDS=0 forces the index form (A/B testing).
@@ -585,7 +567,6 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     D.atlas_h = p->atlas_height;
     D.atlas_layers = p->atlas ? p->atlas_layer_count : 0;
     D.atlas_tiled = s->atlas_tiled ? 1u : 0u;
-    D.fast_div = FastDivBoxes(p) ? 1u : 0u;
     s->mats = SceneMaterialMask(p);
     uint32_t types = s->mats & (PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_TRANSLUCENT | PT_MATS_OPENPBR);
     D.mat_classes = (types & (types - 1)) != 0 ? 1u : 0u;   // more than one material type
