@@ -313,7 +313,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak" if (shard == "samples" and world > 1) else "strong",
+        "scaling": "weak" if shard == "samples" else "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": f"synthetic (procedural {info.mesh_face_count}-triangle room mesh + 1024^2 texture; "
