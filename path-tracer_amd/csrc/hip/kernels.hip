@@ -1164,15 +1164,20 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
     // state is read and written by slot (gathers within the tile's records).
     const uint32_t base = tile * 256;
 #if PT_SHADE_ORDER
+    // The position is the ray's own (slotof inverts TileOrder's slot ->
+    // position map), so the ray / hit / uv records load from it directly,
+    // beside the slotof lookup instead of after a pos[s] lookup.
     const uint64_t* om = L.outcome + (size_t)tile * (4 * PT_OUTCOME_CLASSES);
-    uint32_t s = base | L.slotof[base | (S.mat_classes ? ShadePosition(om, threadIdx.x)
-                                                      : ShadePosition2(om + 4 * (PT_OUTCOME_CLASSES - 1), threadIdx.x))];
+    const uint32_t pq = S.mat_classes ? ShadePosition(om, threadIdx.x)
+                                      : ShadePosition2(om + 4 * (PT_OUTCOME_CLASSES - 1), threadIdx.x);
+    uint32_t s = base | L.slotof[base | pq];
+    const uint32_t p16 = pq << 8;   // RayPos(s, p16) == base | pq (shade -1 % vs gathering pos[s])
 #else
     uint32_t s = base | threadIdx.x;
+    uint32_t p16 = L.pos[s];
 #endif
     uint32_t x, y;
     bool valid = SlotPixel(F, s, x, y);
-    uint32_t p16 = L.pos[s];
     pt3 O = v3s(0), V = v3s(0);
     bool completed = false;
     if (valid) {
