@@ -861,9 +861,9 @@ struct ray_source_slots {
         D = PT_HIT_TIME_LIMIT;
         return true;
     }
-    PT_DEV void store(uint32_t s, const lane_state& Ln) const
+    PT_DEV void store(uint32_t s, const lane_state& Ln, bool vidx21) const
     {
-        L.hit[s] = make_float4(Ln.Time, __uint_as_float(Ln.Shape), __uint_as_float(Ln.Prim), Ln.C.x);
+        L.hit[s] = CompactHit(Ln, vidx21);
         L.uv[s] = make_float2(Ln.C.y, Ln.C.z);
     }
     // ShadeOrder: each wave, once all its rays are traced, stores one ballot
@@ -901,9 +901,9 @@ struct ray_source_arrays {
         D = dur[i];
         return true;
     }
-    PT_DEV void store(uint32_t i, const lane_state& Ln) const
+    PT_DEV void store(uint32_t i, const lane_state& Ln, bool vidx21) const
     {
-        hit[i] = make_float4(Ln.Time, __uint_as_float(Ln.Shape), __uint_as_float(Ln.Prim), Ln.C.x);
+        hit[i] = CompactHit(Ln, vidx21);
         hc[i] = make_float2(Ln.C.y, Ln.C.z);
     }
 };
@@ -953,7 +953,7 @@ PT_DEV void ExtendRay(const dscene& S, const Src& src, tstack<SPILL, CAP, E>& st
             while (!LaneStep<SPILL, CAP, Src, no_stats, true, E>(S, Ln, st, src, slot, ns)) {}
 #endif
         }
-        src.store(slot, Ln);
+        src.store(slot, Ln, S.vidx21 != 0);
         if (Ln.Shape == SHAPE_INDEX_NONE) {
             cls = 4;
         } else if (S.mat_classes) {
@@ -1097,7 +1097,7 @@ __global__ __launch_bounds__(256) void extend_stats_kernel(dscene S, Src src, ui
         LaneBegin(S, Ln, O, V, D);
         if (S.g.ShapeCount != 0)
             while (!LaneStep<SPILL, CAP, Src, lane_stats, true, E>(S, Ln, st, src, slot, ss)) {}
-        src.store(slot, Ln);
+        src.store(slot, Ln, S.vidx21 != 0);
     }
     if (steps && slot < n) steps[slot] = ss.steps;   // per position (0: no ray)
     uint32_t v[14] = {WaveSum(ray), WaveSum(ss.steps), WaveMax(ss.steps) * 64u, WaveSum(ss.internals),
@@ -1127,7 +1127,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(dscene S, uint32_t n, con
     uint32_t Material;
     pt3 N, TX;
     pt2 UV;
-    HitAttributes(S, Shape, __float_as_uint(h.z), v3(h.w, c.x, c.y), Material, N, TX, UV);
+    HitAttributesRecord(S, Shape, h, c, Material, N, TX, UV);
     rec[i] = make_float4(h.x, __uint_as_float((Shape << 16) | Material), __uint_as_float(PackUnitVector(N)),
                          __uint_as_float(PackUnitVector(TX)));
     uv[i] = make_float2(UV.x, UV.y);
@@ -1214,7 +1214,7 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
         if (HitShape != SHAPE_INDEX_NONE) {
             float2 c = L.uv[q];
             pt3 N, TX;
-            HitAttributes(S, HitShape, __float_as_uint(h.z), v3(h.w, c.x, c.y), HitMaterial, N, TX, UV);
+            HitAttributesRecord(S, HitShape, h, c, HitMaterial, N, TX, UV);
             HitMaterial &= 0xFFFFu;
             HitShape &= 0xFFFFu;
             HitTime = h.x;

@@ -39,6 +39,7 @@ struct dscene {
     uint32_t blas_firstbits;       // format 2: bits of a leaf's first face index (count above them)
     uint32_t stack16;              // every stack entry fits 16 bits: extend runs the u16-stack kernel
     uint32_t mat_classes;          // shapes use more than one material type: extend classes hits by type
+    uint32_t vidx21;               // every vertex index fits 21 bits: hit records carry a face's vertex indices
 };
 
 struct ray { pt3 Origin; pt3 Velocity; float Duration; };

@@ -570,6 +570,13 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     s->mats = SceneMaterialMask(p);
     uint32_t types = s->mats & (PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_TRANSLUCENT | PT_MATS_OPENPBR);
     D.mat_classes = (types & (types - 1)) != 0 ? 1u : 0u;   // more than one material type
+    // Hit records carry a mesh face's vertex indices when every index fits
+    // 21 bits (PackVertexIndices, traverse.hpp); PT_VIDX21=0 forces the
+    // face-index form (A/B testing).
+    {
+        const char* e = getenv("PT_VIDX21");
+        D.vidx21 = (p->mesh_vertex_count <= (1u << 21) && !(e && atoi(e) == 0)) ? 1u : 0u;
+    }
     D.blas_words = BlasWordsPackable(p) ? 1u : 0u;
     D.blas_firstbits = 0;
     D.stack16 = 0;

@@ -60,6 +60,8 @@ struct lane_state {
                          // BLAS {FaceBeginOrNodeIndex, FaceEndIndex}
     uint32_t dT, dB;     // TLAS / BLAS stack depths (<= 32 each)
     uint32_t blas;       // shape index of the mesh being traversed, NONE at TLAS level
+    uint32_t HA, HB;     // hit's mesh face vertex indices, 3 x 21 bits (PackVertexIndices);
+                         // an analytic shape's hit: HA = C.x (CompactHit)
 };
 
 PT_DEV void SetLevelRay(const dscene& S, lane_state& L, pt3 O, pt3 V)
@@ -80,6 +82,8 @@ PT_DEV void LaneBegin(const dscene& S, lane_state& L, pt3 O, pt3 V, float Durati
     L.Shape = SHAPE_INDEX_NONE;
     L.Prim = 0;
     L.C = v3s(0);
+    L.HA = 0;
+    L.HB = 0;
     L.dT = 0;
     L.dB = 0;
     L.blas = SHAPE_INDEX_NONE;
@@ -107,6 +111,8 @@ PT_DEV void IntersectAnalytic(int32_t Type, pt3 O, pt3 V, uint32_t ShapeIndex, l
         L.Shape = ShapeIndex;
         L.Prim = 0;
         L.C = O + V * T;
+        L.HA = __float_as_uint(L.C.x);
+        L.HB = 0;
     } else if (Type == PT_SHAPE_TYPE_SPHERE) {
         float Vv = dot(V, V);
         float P = dot(O, V);
@@ -123,6 +129,8 @@ PT_DEV void IntersectAnalytic(int32_t Type, pt3 O, pt3 V, uint32_t ShapeIndex, l
         L.Shape = ShapeIndex;
         L.Prim = 0;
         L.C = O + V * L.Time;
+        L.HA = __float_as_uint(L.C.x);
+        L.HB = 0;
     } else if (Type == PT_SHAPE_TYPE_CUBE) {
         pt3 Mn = (v3s(-1) - O) / V;
         pt3 Mx = (v3s(+1) - O) / V;
@@ -138,6 +146,8 @@ PT_DEV void IntersectAnalytic(int32_t Type, pt3 O, pt3 V, uint32_t ShapeIndex, l
         L.Shape = ShapeIndex;
         L.Prim = 0;
         L.C = O + V * T;
+        L.HA = __float_as_uint(L.C.x);
+        L.HB = 0;
     }
 }
 
@@ -147,7 +157,24 @@ PT_DEV void IntersectAnalytic(int32_t Type, pt3 O, pt3 V, uint32_t ShapeIndex, l
 // Position0`, subtracted once on the host at upload in the same IEEE
 // arithmetic, so every later operation sees identical operands.
 // The test itself: miss flag, T and the coordinates U, W; L is only read.
-PT_DEV bool FaceTest(const dscene& S, uint32_t F, const lane_state& L, bool valid, float& T, float& U, float& W)
+// A face's three vertex indices in 64 bits (21 bits each; dscene::vidx21
+// scenes, whose vertex count fits): the hit record carries them to shade,
+// which then reads the vertices without first reading the face.
+PT_DEV void PackVertexIndices(uint32_t v0, uint32_t v1, uint32_t v2, uint32_t& A, uint32_t& B)
+{
+    A = v0 | (v1 << 21);
+    B = (v1 >> 11) | (v2 << 10);
+}
+
+PT_DEV void UnpackVertexIndices(uint32_t A, uint32_t B, uint32_t& v0, uint32_t& v1, uint32_t& v2)
+{
+    v0 = A & 0x1FFFFFu;
+    v1 = (A >> 21) | ((B & 0x3FFu) << 11);
+    v2 = B >> 10;
+}
+
+PT_DEV bool FaceTest(const dscene& S, uint32_t F, const lane_state& L, bool valid, float& T, float& U, float& W,
+                     uint32_t& VA, uint32_t& VB)
 {
     // valid == false (an empty leaf): face 0 is read and the test forced to
     // miss, instead of a branch around the call.
@@ -157,6 +184,7 @@ PT_DEV bool FaceTest(const dscene& S, uint32_t F, const lane_state& L, bool vali
     pt3 P0 = xyz(a);
     pt3 Edge1 = xyz(b);
     pt3 Edge2 = xyz(c);
+    PackVertexIndices(__float_as_uint(a.w), __float_as_uint(b.w), __float_as_uint(c.w), VA, VB);
     // Every quantity is evaluated with the reference's operations and
     // operand order; its early returns become one predicate (no value
     // depends on which test failed first), so the exits collapse into a
@@ -181,12 +209,15 @@ PT_DEV bool FaceTest(const dscene& S, uint32_t F, const lane_state& L, bool vali
 PT_DEV void LaneMeshFace(const dscene& S, uint32_t F, lane_state& L, bool valid = true)
 {
     float T, U, W;
-    bool miss = FaceTest(S, F, L, valid, T, U, W);
+    uint32_t VA, VB;
+    bool miss = FaceTest(S, F, L, valid, T, U, W, VA, VB);
     // Selects, not a branch: the hit registers are updated in place (a
     // conditional update made the compiler keep and copy a second set).
     L.Time = miss ? L.Time : T;
     L.Shape = miss ? L.Shape : 0xFFFFFFFEu;
     L.Prim = miss ? L.Prim : F;
+    L.HA = miss ? L.HA : VA;
+    L.HB = miss ? L.HB : VB;
     L.C = v3(miss ? L.C.x : 1 - U - W, miss ? L.C.y : U, miss ? L.C.z : W);
 }
 
@@ -422,12 +453,12 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP, SE>& st,
         // other half's lanes.
         bool fmiss = true;
         float fT, fU, fW, TA, TB;
-        uint32_t aw0, aw1, bw0, bw1;
+        uint32_t aw0, aw1, bw0, bw1, fVA, fVB;
         uint32_t pair = L.na;   // child pair whose decision the join applies
-        asm("" : "=v"(fT), "=v"(fU), "=v"(fW), "=v"(TA), "=v"(TB));
+        asm("" : "=v"(fT), "=v"(fU), "=v"(fW), "=v"(TA), "=v"(TB), "=v"(fVA), "=v"(fVB));
         asm("" : "=v"(aw0), "=v"(aw1), "=v"(bw0), "=v"(bw1));
         if (face) {
-            fmiss = FaceTest(S, L.na, L, L.na < L.nb, fT, fU, fW);   // (an empty leaf tests nothing)
+            fmiss = FaceTest(S, L.na, L, L.na < L.nb, fT, fU, fW, fVA, fVB);   // (an empty leaf tests nothing)
             ss.face_step(L.na + 1 >= L.nb);
         } else {
             ss.node(true);
@@ -465,6 +496,8 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP, SE>& st,
         L.Time = fmiss ? L.Time : fT;
         L.Shape = fmiss ? L.Shape : 0xFFFFFFFEu;
         L.Prim = fmiss ? L.Prim : L.na;
+        L.HA = fmiss ? L.HA : fVA;
+        L.HB = fmiss ? L.HB : fVB;
         L.C = v3(fmiss ? L.C.x : 1 - fU - fW, fmiss ? L.C.y : fU, fmiss ? L.C.z : fW);
         // Internal node: the reference's three-way decision (scene.glsl.inc:366-392).
         // (The child set aside is pushed iff its own time is finite: one
@@ -546,9 +579,43 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP, SE>& st,
     return TlasStep(S, L, st, src, slot, ss);
 }
 
-// Hit attribute reconstruction (scene.glsl.inc:535-608).
+// The compact hit record extend stores for shade: {Time, Shape, z, w} and
+// {C.y, C.z}.  In a vidx21 scene z, w are a mesh face's packed vertex indices
+// and C.x = 1 - C.y - C.z is re-evaluated by the reader (the face test's own
+// expression on the same operands), or for an analytic shape z = C.x;
+// otherwise z = Prim, w = C.x.
+PT_DEV float4 CompactHit(const lane_state& Ln, bool vidx21)
+{
+    return make_float4(Ln.Time, __uint_as_float(Ln.Shape), __uint_as_float(vidx21 ? Ln.HA : Ln.Prim),
+                       vidx21 ? __uint_as_float(Ln.HB) : Ln.C.x);
+}
+
+// Hit attribute reconstruction (scene.glsl.inc:535-608).  Mesh faces: the
+// vertex indices come packed in the hit record (vidx21) or from the face.
+PT_DEV void HitAttributesV(const dscene& S, uint32_t ShapeIndex, bool packed, uint32_t Z, uint32_t Wd, pt3 C,
+                           uint32_t& Material, pt3& Normal, pt3& TangentX, pt2& UV);
+
 PT_DEV void HitAttributes(const dscene& S, uint32_t ShapeIndex, uint32_t Prim, pt3 C, uint32_t& Material, pt3& Normal,
                           pt3& TangentX, pt2& UV)
+{
+    HitAttributesV(S, ShapeIndex, false, Prim, 0u, C, Material, Normal, TangentX, UV);
+}
+
+// From a compact hit record (h = {Time, Shape, z, w}, c = {C.y, C.z}).
+PT_DEV void HitAttributesRecord(const dscene& S, uint32_t ShapeIndex, float4 h, float2 c, uint32_t& Material,
+                                pt3& Normal, pt3& TangentX, pt2& UV)
+{
+    const bool mesh = S.shapes[ShapeIndex].Type == PT_SHAPE_TYPE_MESH_INSTANCE;
+    if (S.vidx21) {
+        pt3 C = mesh ? v3(1 - c.x - c.y, c.x, c.y) : v3(h.z, c.x, c.y);
+        HitAttributesV(S, ShapeIndex, true, __float_as_uint(h.z), __float_as_uint(h.w), C, Material, Normal, TangentX, UV);
+    } else {
+        HitAttributesV(S, ShapeIndex, false, __float_as_uint(h.z), 0u, v3(h.w, c.x, c.y), Material, Normal, TangentX, UV);
+    }
+}
+
+PT_DEV void HitAttributesV(const dscene& S, uint32_t ShapeIndex, bool packed, uint32_t Z, uint32_t Wd, pt3 C,
+                           uint32_t& Material, pt3& Normal, pt3& TangentX, pt2& UV)
 {
     const pt_packed_shape* Shape = &S.shapes[ShapeIndex];
     Material = Shape->MaterialIndex;
@@ -556,11 +623,16 @@ PT_DEV void HitAttributes(const dscene& S, uint32_t ShapeIndex, uint32_t Prim, p
     const float* To = Shape->Transform.To;
     const float* From = Shape->Transform.From;
     if (Type == PT_SHAPE_TYPE_MESH_INSTANCE) {
-        const float4* Fp = S.mesh_faces + 3 * (size_t)Prim;
-        float4 f0 = Fp[0], f1 = Fp[1], f2 = Fp[2];
-        uint2 V0 = S.mesh_vertices[__float_as_uint(f0.w)];
-        uint2 V1 = S.mesh_vertices[__float_as_uint(f1.w)];
-        uint2 V2 = S.mesh_vertices[__float_as_uint(f2.w)];
+        uint32_t i0, i1, i2;
+        if (packed) {
+            UnpackVertexIndices(Z, Wd, i0, i1, i2);
+        } else {
+            const float4* Fp = S.mesh_faces + 3 * (size_t)Z;   // Z = Prim
+            i0 = __float_as_uint(Fp[0].w); i1 = __float_as_uint(Fp[1].w); i2 = __float_as_uint(Fp[2].w);
+        }
+        uint2 V0 = S.mesh_vertices[i0];
+        uint2 V1 = S.mesh_vertices[i1];
+        uint2 V2 = S.mesh_vertices[i2];
         pt3 N = SafeNormalize(UnpackUnitVector(V0.x) * C.x + UnpackUnitVector(V1.x) * C.y + UnpackUnitVector(V2.x) * C.z);
         Normal = TransformNormal(N, From);
         TangentX = ComputeTangentVector(Normal);
