@@ -383,3 +383,18 @@ def test_two_process_sample_shards_equal_summed_renders(pt, dev, tmp_path):
     assert np.array_equal(bits(got["accum2"]), bits(want[1]))
     ds.close()
     s.close()
+
+
+@pytest.mark.parametrize("vidx21", ["0", "1"])
+def test_hit_record_forms_bit_exact(pt, dev, monkeypatch, vidx21):
+    """Both compact hit-record forms (packed vertex indices, the default for
+    scenes whose vertex indices fit 21 bits, and the face-index form that
+    larger scenes use; PT_VIDX21=0 forces it) give the oracle's state and
+    image, meshes and analytic shapes alike (C5 mixes both)."""
+    monkeypatch.setenv("PT_VIDX21", vidx21)
+    for cfg, W, H in ((3, 160, 96), (5, 128, 64)):
+        s = pt.Scene.config(cfg)
+        gs, os_, ga, oa = render_pair(pt, dev, cfg, W, H, [2, 1, 1], scene=s)
+        compare_state(gs, os_)
+        assert np.array_equal(bits(ga), bits(oa))
+        s.close()
