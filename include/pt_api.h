@@ -232,12 +232,14 @@ int         ptReadPreviewAOVs(pt_device* device, pt_preview* context, pt_preview
 int ptTraceRays(pt_device* device, pt_scene* scene, uint32_t n, const float* origins,
                 const uint32_t* packed_velocities, const float* durations, pt_hit_record* out);
 
-/* Diagnostic: evaluates the extend kernel's exact fast division (FMA-corrected
- * reciprocal) against IEEE division on n device-generated operand pairs and
- * returns the number of bit mismatches (must be 0). */
+/* Diagnostic: evaluates the device's exact fast division helper (XDiv: an
+ * FMA-corrected reciprocal, no longer on the traversal path since the slab
+ * test's reciprocal convention) against IEEE division on n
+ * device-generated operand pairs; returns the number of bit mismatches
+ * (must be 0). */
 int ptCheckFastDivision(pt_device* device, uint64_t n, uint32_t seed, uint64_t* mismatches);
 
-/* Diagnostic: evaluates the traversal's fast reciprocal (hardware rcp + one
+/* Diagnostic: evaluates the device's fast reciprocal (hardware rcp + one
  * FMA Newton step) on every float d with 2^-126 <= |d| < 2^126 against the
  * IEEE quotient 1.0f / d; returns the number of bit mismatches (must be 0). */
 int ptCheckFastReciprocal(pt_device* device, uint64_t* mismatches);

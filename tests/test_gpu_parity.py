@@ -51,8 +51,9 @@ def random_rays(arrays, n, seed):
         hi = np.minimum(hi, mx + 1.0)
     o = rng.uniform(lo, hi, size=(n, 3)).astype(np.float32)
     d = rng.normal(size=(n, 3))
-    # exercise the IEEE slab-division path: axis-aligned directions (zero
-    # velocity components), zero and tiny origin components
+    # exercise the slab test's special cases: axis-aligned directions (zero
+    # velocity components: infinite reciprocals, 0 * inf = NaN planes), zero
+    # and tiny origin components
     axes = np.array([[1, 0, 0], [-1, 0, 0], [0, 1, 0], [0, -1, 0], [0, 0, 1], [0, 0, -1],
                      [0.6, 0.8, 0], [0, -0.6, 0.8], [1e-20, 1, 0.5]])
     d[: 9 * 32] = np.repeat(axes, 32, axis=0)
@@ -294,7 +295,7 @@ def test_bad_camera_index_rejected(pt, dev):
 
 
 def test_fast_division_matches_ieee(pt, dev):
-    """The extend kernel's FMA-corrected division is bit-identical to a / b."""
+    """The FMA-corrected division helper (XDiv) is bit-identical to a / b."""
     for seed in (1, 2, 3, 4):
         assert dev.check_fast_division(1 << 28, seed) == 0
 
