@@ -6,7 +6,8 @@
 // decode RGBE to linear floats with alpha 1.  This decoder follows the PNG
 // (ISO/IEC 15948) and Radiance RGBE specifications and applies those
 // conversions; it reads JPEG (jpeg.cpp), PNG of every colour type / bit depth (incl. palette,
-// tRNS and Adam7 interlacing), BMP, TGA and RLE or flat RGBE .hdr.
+// tRNS and Adam7 interlacing), BMP, GIF (first frame), binary PNM, TGA and RLE
+// or flat RGBE .hdr.
 #include "image.hpp"
 
 #include <zlib.h>
@@ -472,18 +473,284 @@ bool DecodeBMP(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_
     return true;
 }
 
-// JPEG, PNG, BMP or TGA (the format without a signature, tried last as stb
-// does; stbi__load_main tries JPEG first: an SOI marker, after any 0xFF fill).
+// A byte stream with stbi__get8's end-of-data behaviour (0 past the end).
+struct byte_reader {
+    const std::vector<uint8_t>& f;
+    size_t pos = 0;
+    bool eof() const { return pos >= f.size(); }
+    uint8_t get8() { return pos < f.size() ? f[pos++] : 0; }
+    uint32_t get16le() { uint32_t a = get8(); return a | (uint32_t)get8() << 8; }
+    void skip(size_t n) { pos = std::min(f.size(), pos + n); }
+};
+
+// Binary PNM (P5 grey / P6 RGB), as stbi__pnm_info / stbi__pnm_load
+// (stb_image 2.29, the reference's copy): header integers separated by
+// whitespace and '#' comments, the single byte after maxval ends the header;
+// maxval only selects 8- or 16-bit samples (it does not scale them).  16-bit
+// samples are read in host byte order and reduced by >> 8
+// (stbi__convert_16_to_8), so the second byte of each big-endian sample is
+// the result.  `matched` is false when the signature is not P5 / P6.
+bool DecodePNM(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_t>& rgba8, std::string& err,
+               bool& matched)
+{
+    byte_reader r{f};
+    char p = (char)r.get8(), t = (char)r.get8();
+    matched = p == 'P' && (t == '5' || t == '6');
+    if (!matched) return false;
+    const int comp = t == '6' ? 3 : 1;
+    auto space = [](char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\v' || c == '\f' || c == '\r'; };
+    char c = (char)r.get8();
+    auto skip_ws = [&]() {
+        for (;;) {
+            while (!r.eof() && space(c)) c = (char)r.get8();
+            if (r.eof() || c != '#') break;
+            while (!r.eof() && c != '\n' && c != '\r') c = (char)r.get8();
+        }
+    };
+    bool overflow = false;
+    auto integer = [&]() {
+        int v = 0;
+        while (!r.eof() && c >= '0' && c <= '9') {
+            v = v * 10 + (c - '0');
+            c = (char)r.get8();
+            if (v > 214748364 || (v == 214748364 && c > '7')) { overflow = true; return 0; }
+        }
+        return v;
+    };
+    skip_ws();
+    int w = integer();
+    if (w == 0) { err = overflow ? "PNM header integer overflow" : "PNM: invalid width"; return false; }
+    skip_ws();
+    int h = integer();
+    if (h == 0) { err = overflow ? "PNM header integer overflow" : "PNM: invalid height"; return false; }
+    skip_ws();
+    int maxv = integer();
+    if (overflow) { err = "PNM header integer overflow"; return false; }
+    if (maxv > 65535) { err = "PNM: max value > 65535"; return false; }
+    const int bytes = maxv > 255 ? 2 : 1;
+    if (w > (1 << 24) || h > (1 << 24)) { err = "PNM: too large"; return false; }
+    const size_t n = (size_t)w * h;
+    if (f.size() - std::min(f.size(), r.pos) < n * comp * bytes) { err = "PNM file truncated"; return false; }
+    const uint8_t* d = f.data() + r.pos;
+    W = w;
+    H = h;
+    rgba8.resize(n * 4);
+    for (size_t i = 0; i < n; i++) {
+        uint8_t v[3];
+        for (int k = 0; k < comp; k++) v[k] = d[(i * comp + k) * bytes + (bytes - 1)];
+        uint8_t* o = &rgba8[4 * i];
+        o[0] = v[0];
+        o[1] = comp == 3 ? v[1] : v[0];
+        o[2] = comp == 3 ? v[2] : v[0];
+        o[3] = 255;
+    }
+    return true;
+}
+
+// GIF, first frame only, as stbi_load gives it (stbi__gif_load ->
+// stbi__gif_load_next once; stb_image 2.29).  Every behaviour below is that
+// loader's: palettes with the graphic-control transparent entry at alpha 0
+// (pixels of alpha <= 128 are not drawn and stay 0,0,0,0); the LZW stream
+// must start with a clear code, table entries keep being added past 4096
+// (up to 8192) at 12 bits; codes beyond the frame rectangle are dropped;
+// interlaced frames walk rows 0,8,.. 4,.. 2,.. 1,..; and on the first frame,
+// when the background index is not 0, the pixels the frame never touched
+// take the global palette's background entry copied in its stored B,G,R
+// order with alpha 255.
+bool DecodeGIF(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_t>& rgba8, std::string& err)
+{
+    byte_reader r{f};
+    if (r.get8() != 'G' || r.get8() != 'I' || r.get8() != 'F' || r.get8() != '8') { err = "not GIF"; return false; }
+    uint8_t version = r.get8();
+    if ((version != '7' && version != '9') || r.get8() != 'a') { err = "not GIF"; return false; }
+    const uint32_t gw = r.get16le(), gh = r.get16le();
+    const uint32_t flags = r.get8(), bgindex = r.get8();
+    r.get8();   // aspect ratio
+    if (gw > (1u << 24) || gh > (1u << 24)) { err = "GIF: too large"; return false; }
+    uint8_t pal[256][4] = {}, lpal[256][4] = {};   // B, G, R, A as stb stores them
+    auto colortable = [&](uint8_t (*t)[4], int entries, int transp) {
+        for (int i = 0; i < entries; i++) {
+            t[i][2] = r.get8();
+            t[i][1] = r.get8();
+            t[i][0] = r.get8();
+            t[i][3] = transp == i ? 0 : 255;
+        }
+    };
+    if (flags & 0x80) colortable(pal, 2 << (flags & 7), -1);
+    const size_t pcount = (size_t)gw * gh;
+    if (pcount == 0) { err = "GIF: empty image"; return false; }
+    std::vector<uint8_t> out(4 * pcount, 0), history(pcount, 0);
+    int transparent = -1;
+    uint32_t eflags = 0;
+    for (;;) {
+        int tag = r.get8();
+        if (tag == 0x2C) {   // image descriptor
+            uint32_t x = r.get16le(), y = r.get16le(), w = r.get16le(), h = r.get16le();
+            if (x + w > gw || y + h > gh) { err = "GIF: bad image descriptor"; return false; }
+            const int64_t line = (int64_t)gw * 4;
+            const int64_t start_x = (int64_t)x * 4, start_y = (int64_t)y * line;
+            const int64_t max_x = start_x + (int64_t)w * 4, max_y = start_y + (int64_t)h * line;
+            int64_t cur_x = start_x, cur_y = start_y;
+            if (w == 0) cur_y = max_y;
+            uint32_t lflags = r.get8();
+            int64_t step;
+            int parse;
+            if (lflags & 0x40) { step = 8 * line; parse = 3; } else { step = line; parse = 0; }
+            uint8_t (*table)[4];
+            if (lflags & 0x80) {
+                colortable(lpal, 2 << (lflags & 7), (eflags & 0x01) ? transparent : -1);
+                table = lpal;
+            } else if (flags & 0x80) {
+                table = pal;
+            } else {
+                err = "GIF: missing color table";
+                return false;
+            }
+            // stbi__process_gif_raster
+            const uint32_t lzw_cs = r.get8();
+            if (lzw_cs > 12) { err = "GIF: bad LZW code size"; return false; }
+            struct code { int16_t prefix; uint8_t first, suffix; };
+            std::vector<code> codes(8192);
+            const int32_t clear = 1 << lzw_cs;
+            for (int32_t i = 0; i < clear; i++) codes[(size_t)i] = {-1, (uint8_t)i, (uint8_t)i};
+            bool first = true;
+            int32_t codesize = (int32_t)lzw_cs + 1, codemask = (1 << codesize) - 1;
+            int32_t avail = clear + 2, oldcode = -1, bits = 0, valid_bits = 0, len = 0;
+            std::vector<uint8_t> chain;
+            // stbi__out_gif_code: the code's string, prefix first.
+            auto emit = [&](int32_t c) {
+                chain.clear();
+                for (int32_t k = c; k >= 0; k = codes[(size_t)k].prefix) chain.push_back(codes[(size_t)k].suffix);
+                for (size_t j = chain.size(); j-- > 0;) {
+                    if (cur_y >= max_y) return;
+                    const int64_t idx = cur_x + cur_y;
+                    history[(size_t)(idx / 4)] = 1;
+                    const uint8_t* cc = table[chain[j]];
+                    if (cc[3] > 128) {
+                        uint8_t* o = &out[(size_t)idx];
+                        o[0] = cc[2]; o[1] = cc[1]; o[2] = cc[0]; o[3] = cc[3];
+                    }
+                    cur_x += 4;
+                    if (cur_x >= max_x) {
+                        cur_x = start_x;
+                        cur_y += step;
+                        while (cur_y >= max_y && parse > 0) {
+                            step = ((int64_t)1 << parse) * line;
+                            cur_y = start_y + (step >> 1);
+                            --parse;
+                        }
+                    }
+                }
+            };
+            for (;;) {
+                if (valid_bits < codesize) {
+                    if (len == 0) {
+                        len = r.get8();
+                        if (len == 0) goto frame_done;
+                    }
+                    --len;
+                    bits |= (int32_t)r.get8() << valid_bits;
+                    valid_bits += 8;
+                    continue;
+                }
+                int32_t c = bits & codemask;
+                bits >>= codesize;
+                valid_bits -= codesize;
+                if (c == clear) {
+                    codesize = (int32_t)lzw_cs + 1;
+                    codemask = (1 << codesize) - 1;
+                    avail = clear + 2;
+                    oldcode = -1;
+                    first = false;
+                } else if (c == clear + 1) {   // end of information: skip the rest of the data
+                    r.skip((size_t)len);
+                    while ((len = r.get8()) > 0) r.skip((size_t)len);
+                    goto frame_done;
+                } else if (c <= avail) {
+                    if (first) { err = "GIF: no clear code"; return false; }
+                    if (oldcode >= 0) {
+                        code& nc = codes[(size_t)avail++];
+                        if (avail > 8192) { err = "GIF: too many codes"; return false; }
+                        nc.prefix = (int16_t)oldcode;
+                        nc.first = codes[(size_t)oldcode].first;
+                        nc.suffix = (c == avail) ? nc.first : codes[(size_t)c].first;
+                    } else if (c == avail) {
+                        err = "GIF: illegal code in raster";
+                        return false;
+                    }
+                    emit(c);
+                    if ((avail & codemask) == 0 && avail <= 0x0FFF) {
+                        codesize++;
+                        codemask = (1 << codesize) - 1;
+                    }
+                    oldcode = c;
+                } else {
+                    err = "GIF: illegal code in raster";
+                    return false;
+                }
+            }
+        frame_done:
+            if (bgindex > 0)
+                for (size_t i = 0; i < pcount; i++)
+                    if (!history[i]) {
+                        pal[bgindex][3] = 255;
+                        std::memcpy(&out[4 * i], pal[bgindex], 4);
+                    }
+            W = (int)gw;
+            H = (int)gh;
+            rgba8.swap(out);
+            return true;
+        } else if (tag == 0x21) {   // extension
+            int ext = r.get8();
+            if (ext == 0xF9) {   // graphic control
+                int len = r.get8();
+                if (len == 4) {
+                    eflags = r.get8();
+                    r.get16le();   // delay
+                    if (transparent >= 0) pal[transparent][3] = 255;
+                    if (eflags & 0x01) {
+                        transparent = r.get8();
+                        pal[transparent][3] = 0;
+                    } else {
+                        r.skip(1);
+                        transparent = -1;
+                    }
+                } else {
+                    r.skip((size_t)len);
+                    continue;   // (stb leaves the sub-block terminator to the tag loop)
+                }
+            }
+            int len;
+            while ((len = r.get8()) != 0) r.skip((size_t)len);
+        } else if (tag == 0x3B) {   // trailer before any frame
+            err = "GIF: no image";
+            return false;
+        } else {
+            err = "GIF: unknown block";
+            return false;
+        }
+    }
+}
+
+// The stb_image formats LoadTexture's stbi_loadf reads, in stbi__load_main's
+// order for the signatures that could collide (PNG, BMP, GIF, JPEG, PNM; TGA,
+// which has none, last).  JPEG: an SOI marker after any 0xFF fill.  Not read:
+// PSD and Softimage PIC.
 bool DecodeLDR(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_t>& rgba8, std::string& err)
 {
     static const uint8_t png_sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+    if (f.size() >= 8 && std::memcmp(f.data(), png_sig, 8) == 0) return DecodePNG(f, W, H, rgba8, err);
+    if (f.size() >= 2 && f[0] == 'B' && f[1] == 'M') return DecodeBMP(f, W, H, rgba8, err);
+    if (f.size() >= 6 && std::memcmp(f.data(), "GIF8", 4) == 0 && (f[4] == '7' || f[4] == '9') && f[5] == 'a')
+        return DecodeGIF(f, W, H, rgba8, err);
     size_t k = 0;
     while (k < f.size() && f[k] == 0xFF) k++;
     if (k >= 1 && k < f.size() && f[k] == 0xD8) return DecodeJPEG(f, W, H, rgba8, err);
-    if (f.size() >= 8 && std::memcmp(f.data(), png_sig, 8) == 0) return DecodePNG(f, W, H, rgba8, err);
-    if (f.size() >= 2 && f[0] == 'B' && f[1] == 'M') return DecodeBMP(f, W, H, rgba8, err);
+    bool pnm = false;
+    if (DecodePNM(f, W, H, rgba8, err, pnm)) return true;
+    if (pnm) return false;
     if (DecodeTGA(f, W, H, rgba8, err)) return true;
-    err = "unsupported image format (JPEG, PNG, BMP, TGA, Radiance HDR)";
+    err = "unsupported image format (JPEG, PNG, BMP, GIF, PNM, TGA, Radiance HDR)";
     return false;
 }
 

@@ -213,11 +213,11 @@ def test_bmp_palette(pt, tmp_path, bpp, hsz):
 
 
 def test_unknown_format_rejected(pt, tmp_path):
-    (tmp_path / "x.gif").write_bytes(b"GIF89a" + b"\0" * 64)
+    (tmp_path / "x.psd").write_bytes(b"8BPS" + b"\0" * 64)      # Photoshop: a stb format this build does not read
     (tmp_path / "x.jpg").write_bytes(b"\xff\xd8\xff\xe0" + b"\0" * 64)   # SOI, then an APP0 of length 0
     s = pt.Scene.empty()
     with pytest.raises(OSError, match="unsupported image format"):
-        s.load_texture(tmp_path / "x.gif", 0)
+        s.load_texture(tmp_path / "x.psd", 0)
     with pytest.raises(OSError, match="JPEG"):
         s.load_texture(tmp_path / "x.jpg", 0)
     s.close()
