@@ -6,8 +6,8 @@
 // decode RGBE to linear floats with alpha 1.  This decoder follows the PNG
 // (ISO/IEC 15948) and Radiance RGBE specifications and applies those
 // conversions; it reads JPEG (jpeg.cpp), PNG of every colour type / bit depth (incl. palette,
-// tRNS and Adam7 interlacing), BMP, GIF (first frame), binary PNM, TGA and RLE
-// or flat RGBE .hdr.
+// tRNS and Adam7 interlacing), BMP, GIF (first frame), PSD (composite), binary
+// PNM, TGA and RLE or flat RGBE .hdr.
 #include "image.hpp"
 
 #include <zlib.h>
@@ -732,10 +732,95 @@ bool DecodeGIF(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_
     }
 }
 
+// Photoshop PSD, the composited image, as stbi__psd_load at 8 bits per
+// channel (stbi_loadf's path): RGB colour mode only, 8- or 16-bit samples
+// (16-bit reduced to the high byte), raw or PackBits RLE planes (RLE is
+// decoded as one byte per sample whatever the depth, as stb does), channels
+// past the fourth ignored, missing ones filled with 0 (alpha 255); with four
+// or more channels the "white matte" is removed from partly transparent
+// pixels by stb's float expression v * (1/a) + 255 * (1 - 1/a), truncated to
+// an integer and stored modulo 256.
+bool DecodePSD(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_t>& rgba8, std::string& err)
+{
+    byte_reader r{f};
+    auto get16be = [&]() { uint32_t a = r.get8(); return (a << 8) | r.get8(); };
+    auto get32be = [&]() { uint32_t a = get16be(); return (a << 16) | get16be(); };
+    if (get32be() != 0x38425053u) { err = "not PSD"; return false; }
+    if (get16be() != 1) { err = "PSD: unsupported version"; return false; }
+    r.skip(6);
+    const int channels = (int)get16be();
+    if (channels > 16) { err = "PSD: unsupported channel count"; return false; }
+    const int32_t h = (int32_t)get32be(), w = (int32_t)get32be();
+    if (h > (1 << 24) || w > (1 << 24) || h <= 0 || w <= 0) { err = "PSD: bad size"; return false; }
+    const uint32_t depth = get16be();
+    if (depth != 8 && depth != 16) { err = "PSD: bit depth is not 8 or 16"; return false; }
+    if (get16be() != 3) { err = "PSD: not in RGB color mode"; return false; }
+    r.skip(get32be());   // mode data
+    r.skip(get32be());   // image resources
+    r.skip(get32be());   // layer and mask information
+    const uint32_t compression = get16be();
+    if (compression > 1) { err = "PSD: unknown compression"; return false; }
+    const size_t n = (size_t)w * h;
+    std::vector<uint8_t> out(4 * n);
+    if (compression) {
+        r.skip((size_t)h * channels * 2);   // per-row byte counts
+        for (int ch = 0; ch < 4; ch++) {
+            uint8_t* p = out.data() + ch;
+            if (ch >= channels) {
+                for (size_t i = 0; i < n; i++, p += 4) *p = ch == 3 ? 255 : 0;
+                continue;
+            }
+            size_t count = 0;
+            while (count < n) {
+                const size_t nleft = n - count;
+                uint32_t len = r.get8();
+                if (len == 128) continue;
+                if (len < 128) {
+                    len++;
+                    if (len > nleft) { err = "PSD: bad RLE data"; return false; }
+                    count += len;
+                    for (; len; len--, p += 4) *p = r.get8();
+                } else {
+                    len = 257 - len;
+                    if (len > nleft) { err = "PSD: bad RLE data"; return false; }
+                    const uint8_t v = r.get8();
+                    count += len;
+                    for (; len; len--, p += 4) *p = v;
+                }
+            }
+        }
+    } else {
+        for (int ch = 0; ch < 4; ch++) {
+            uint8_t* p = out.data() + ch;
+            if (ch >= channels) {
+                for (size_t i = 0; i < n; i++, p += 4) *p = ch == 3 ? 255 : 0;
+            } else if (depth == 16) {
+                for (size_t i = 0; i < n; i++, p += 4) *p = (uint8_t)(get16be() >> 8);
+            } else {
+                for (size_t i = 0; i < n; i++, p += 4) *p = r.get8();
+            }
+        }
+    }
+    if (channels >= 4)
+        for (size_t i = 0; i < n; i++) {
+            uint8_t* px = &out[4 * i];
+            if (px[3] != 0 && px[3] != 255) {
+                const float a = px[3] / 255.0f;
+                const float ra = 1.0f / a;
+                const float inv_a = 255.0f * (1 - ra);
+                for (int k = 0; k < 3; k++) px[k] = (uint8_t)(int32_t)(px[k] * ra + inv_a);
+            }
+        }
+    W = w;
+    H = h;
+    rgba8.swap(out);
+    return true;
+}
+
 // The stb_image formats LoadTexture's stbi_loadf reads, in stbi__load_main's
-// order for the signatures that could collide (PNG, BMP, GIF, JPEG, PNM; TGA,
-// which has none, last).  JPEG: an SOI marker after any 0xFF fill.  Not read:
-// PSD and Softimage PIC.
+// order for the signatures that could collide (PNG, BMP, GIF, PSD, JPEG, PNM;
+// TGA, which has none, last).  JPEG: an SOI marker after any 0xFF fill.  Not
+// read: Softimage PIC.
 bool DecodeLDR(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_t>& rgba8, std::string& err)
 {
     static const uint8_t png_sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
@@ -743,6 +828,7 @@ bool DecodeLDR(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_
     if (f.size() >= 2 && f[0] == 'B' && f[1] == 'M') return DecodeBMP(f, W, H, rgba8, err);
     if (f.size() >= 6 && std::memcmp(f.data(), "GIF8", 4) == 0 && (f[4] == '7' || f[4] == '9') && f[5] == 'a')
         return DecodeGIF(f, W, H, rgba8, err);
+    if (f.size() >= 4 && std::memcmp(f.data(), "8BPS", 4) == 0) return DecodePSD(f, W, H, rgba8, err);
     size_t k = 0;
     while (k < f.size() && f[k] == 0xFF) k++;
     if (k >= 1 && k < f.size() && f[k] == 0xD8) return DecodeJPEG(f, W, H, rgba8, err);
@@ -750,7 +836,7 @@ bool DecodeLDR(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_
     if (DecodePNM(f, W, H, rgba8, err, pnm)) return true;
     if (pnm) return false;
     if (DecodeTGA(f, W, H, rgba8, err)) return true;
-    err = "unsupported image format (JPEG, PNG, BMP, GIF, PNM, TGA, Radiance HDR)";
+    err = "unsupported image format (JPEG, PNG, BMP, GIF, PSD, PNM, TGA, Radiance HDR)";
     return false;
 }
 

@@ -213,11 +213,12 @@ def test_bmp_palette(pt, tmp_path, bpp, hsz):
 
 
 def test_unknown_format_rejected(pt, tmp_path):
-    (tmp_path / "x.psd").write_bytes(b"8BPS" + b"\0" * 64)      # Photoshop: a stb format this build does not read
+    pic = b"\x53\x80\xf6\x34" + b"\0" * 84 + b"PICT" + b"\0" * 16
+    (tmp_path / "x.pic").write_bytes(pic)      # Softimage PIC: a stb format this build does not read
     (tmp_path / "x.jpg").write_bytes(b"\xff\xd8\xff\xe0" + b"\0" * 64)   # SOI, then an APP0 of length 0
     s = pt.Scene.empty()
     with pytest.raises(OSError, match="unsupported image format"):
-        s.load_texture(tmp_path / "x.psd", 0)
+        s.load_texture(tmp_path / "x.pic", 0)
     with pytest.raises(OSError, match="JPEG"):
         s.load_texture(tmp_path / "x.jpg", 0)
     s.close()
