@@ -51,13 +51,16 @@ struct dbuf {
     void release() { if (ptr) (void)hipFree(ptr); ptr = nullptr; count = 0; }
     hipError_t upload(const T* src, size_t n)
     {
-        if (n > count) {
+        // An empty array still gets one zeroed element, so that kernels which
+        // read a first record unconditionally (the TLAS root in LaneBegin)
+        // read defined memory in a scene without shapes.
+        if (!ptr || n > count) {
             release();
             hipError_t e = hipMalloc(&ptr, std::max<size_t>(n, 1) * sizeof(T));
             if (e != hipSuccess) { ptr = nullptr; return e; }
             count = n;
         }
-        if (n == 0) return hipSuccess;
+        if (n == 0) return hipMemset(ptr, 0, sizeof(T));
         return hipMemcpy(ptr, src, n * sizeof(T), hipMemcpyHostToDevice);
     }
     hipError_t alloc(size_t n)

@@ -181,7 +181,7 @@ class Scene:
 
     # -- ingestion (scene.cpp:294-313, 601-903) ---------------------------------
     def load_texture(self, path, texture_type=TEXTURE_RAW, name=None):
-        """LoadTexture: PNG, BMP, TGA or Radiance .hdr, stbi_loadf semantics."""
+        """LoadTexture: JPEG, PNG, BMP, GIF, PSD, PNM, TGA or Radiance .hdr, stbi_loadf semantics."""
         L = N.scene_lib()
         t = L.ptsLoadTexture(self._h, str(path).encode(), int(texture_type), name.encode() if name else None)
         if not t:

@@ -34,7 +34,7 @@ import numpy as np
 import pytest
 
 import oracle_lib
-from test_gpu_parity import compare_state, render_pair
+from test_gpu_parity import compare_hits, compare_state, random_rays, render_pair
 
 pytestmark = pytest.mark.gpu
 
@@ -398,3 +398,37 @@ def test_hit_record_forms_bit_exact(pt, dev, monkeypatch, vidx21):
         compare_state(gs, os_)
         assert np.array_equal(bits(ga), bits(oa))
         s.close()
+
+
+def edge_scene(pt, kind):
+    """Scenes at the traversal's edges: no shapes at all (every ray misses;
+    the reference would read an uninitialised node buffer here, so the
+    oracle's all-miss reading is the contract), one analytic shape (the TLAS
+    root is a shape leaf), one single-triangle mesh (the BLAS root is a leaf)."""
+    s = pt.Scene.empty()
+    s.create_entity(pt.ENTITY_CAMERA, position=(0.0, -2.0, 1.0), rotation=(1.2, 0.0, 0.0))
+    if kind == "sphere":
+        s.create_entity(pt.ENTITY_SPHERE, position=(0.0, 0.0, 1.0), scale=(0.5,) * 3)
+    elif kind == "triangle":
+        m = s.create_mesh([[-1, 0, 0], [1, 0, 0], [0, 0, 2]], [[0, 1, 2]])
+        e = s.create_entity(pt.ENTITY_MESH_INSTANCE)
+        s.set_mesh(e, m)
+    s.set_root(skybox_sampling_probability=0.5, skybox_brightness=2.0)
+    s.pack()
+    return s
+
+
+@pytest.mark.parametrize("kind", ["empty", "sphere", "triangle"])
+@pytest.mark.parametrize("W,H", [(1, 1), (37, 21)])
+def test_edge_scenes_bit_exact(pt, dev, kind, W, H):
+    s = edge_scene(pt, kind)
+    gs, os_, ga, oa = render_pair(pt, dev, None, W, H, [2, 1, 1], scene=s)
+    compare_state(gs, os_)
+    assert np.array_equal(ga.view(np.uint32), oa.view(np.uint32))
+    assert oa[..., 3].sum() > 0
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    o, v, d = random_rays(s.arrays(), 4096, seed=71)
+    compare_hits(ds.trace_rays(o, v, d), oracle_lib.trace_rays(s.packs(), o, v, d))
+    ds.close()
+    s.close()
