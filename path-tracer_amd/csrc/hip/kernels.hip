@@ -1026,9 +1026,25 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, 
     };
     for (uint32_t t = threadIdx.x; t < tiles; t += 1024) atomicAdd(&count[key(t)], 1u);
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t sum = 0;
-        for (uint32_t i = 0; i < 512; i++) { uint32_t c = count[i]; count[i] = sum; sum += c; }
+    // Exclusive scan of the 512 buckets: eight waves scan 64 each with
+    // shuffles, then add the totals of the waves before them (a serial scan
+    // by one thread was most of this kernel's 11 us).
+    __shared__ uint32_t wsum[8];
+    uint32_t c = 0, incl = 0;
+    if (threadIdx.x < 512) {
+        c = count[threadIdx.x];
+        incl = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            uint32_t t = (uint32_t)__shfl_up((int)incl, o, 64);
+            if ((threadIdx.x & 63u) >= (uint32_t)o) incl += t;
+        }
+        if ((threadIdx.x & 63u) == 63u) wsum[threadIdx.x >> 6] = incl;
+    }
+    __syncthreads();
+    if (threadIdx.x < 512) {
+        uint32_t before = 0;
+        for (uint32_t w = 0; w < (threadIdx.x >> 6); w++) before += wsum[w];
+        count[threadIdx.x] = before + incl - c;
     }
     __syncthreads();
     for (uint32_t t = threadIdx.x; t < tiles; t += 1024) order[atomicAdd(&count[key(t)], 1u)] = base + t;
