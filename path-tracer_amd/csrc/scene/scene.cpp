@@ -5,7 +5,11 @@
 #include <algorithm>
 #include <cassert>
 #include <cstring>
+#include <array>
+#include <cstdlib>
 #include <functional>
+#include <thread>
+#include <vector>
 
 namespace pth {
 
@@ -56,74 +60,131 @@ void ForEachEntityWithTransform(entity* Entity, const mat4& Outer,
     F(Entity, Transform);
 }
 
-float GetMeshFaceCentroid(mesh* Mesh, uint32_t FaceIndex, int Axis)   // scene.cpp:424-433
+// BuildMeshNode (scene.cpp:435-599): 32-bin centroid SAH per axis.
+//
+// The build is split into SplitMeshNode (one node's bounds, binned SAH and
+// partition: the reference's function body up to its recursion) and two
+// drivers: BuildMeshNode, the reference's sequential recursion, and
+// BuildMeshSubtree, which runs the two children of the top nodes on separate
+// threads and the bounds / centroid-range / binning passes of large nodes
+// over chunks of the face range.  Both give the reference's nodes and face
+// order bit for bit: chunk results merge in chunk order, and Grow, gmin/gmax
+// and std::min/max keep the earlier of equal values exactly as the sequential
+// fold does (so even the signs of zero bounds agree); bin counts are integer
+// sums; the SAH sweep and the partition loop are the reference's, run by one
+// thread per node; and the node array is assembled in the reference's
+// allocation order (a node's two children, then the left child's
+// descendants, then the right child's).
+
+struct bvh_ctx {
+    const std::vector<mesh_vertex>* V;
+    std::vector<mesh_face>* F;
+};
+
+inline float FaceCentroid(const bvh_ctx& C, uint32_t FaceIndex, int Axis)   // GetMeshFaceCentroid, scene.cpp:424-433
 {
     float Centroid = 0.0f;
-    for (uint32_t I = 0; I < 3; I++) {
-        uint32_t VertexIndex = Mesh->Faces[FaceIndex].VertexIndex[I];
-        Centroid += Mesh->Vertices[VertexIndex].Position[Axis];
-    }
+    for (uint32_t I = 0; I < 3; I++) Centroid += (*C.V)[(*C.F)[FaceIndex].VertexIndex[I]].Position[Axis];
     return Centroid / 3.0f;
 }
 
-// BuildMeshNode (scene.cpp:435-599): 32-bin centroid SAH per axis.
-void BuildMeshNode(mesh* Mesh, uint32_t NodeIndex, uint32_t Depth)
-{
-    mesh_node& Node = Mesh->Nodes[NodeIndex];
-    uint32_t FaceCount = Node.FaceEndIndex - Node.FaceBeginIndex;
+constexpr uint32_t BVH_BINS = 32;
+struct bvh_bin { bounds Bounds; uint32_t FaceCount = 0; };
 
-    Node.Bounds = {};
-    for (uint32_t Index = Node.FaceBeginIndex; Index < Node.FaceEndIndex; Index++)
-        for (int J = 0; J < 3; J++) Grow(Node.Bounds, Mesh->Vertices[Mesh->Faces[Index].VertexIndex[J]].Position);
+// Runs body(chunk, begin, end) over `parts` contiguous chunks of [b, e)
+// (chunk 0 on the calling thread).
+template <class Body>
+void ForChunks(uint32_t b, uint32_t e, unsigned parts, Body body)
+{
+    if (parts <= 1) { body(0u, b, e); return; }
+    std::vector<std::thread> pool;
+    uint64_t n = e - b;
+    for (unsigned c = 1; c < parts; c++)
+        pool.emplace_back(body, c, (uint32_t)(b + n * c / parts), (uint32_t)(b + n * (c + 1) / parts));
+    body(0u, b, (uint32_t)(b + n / parts));
+    for (auto& t : pool) t.join();
+}
+
+constexpr uint32_t BVH_PARALLEL_PASS_FACES = 1u << 16;   // below this a node's passes stay on one thread
+
+// One node of BuildMeshNode: bounds, split choice, partition.  Returns the
+// split index, or 0 when the node stays a leaf.
+uint32_t SplitMeshNode(const bvh_ctx& C, mesh_node& Node, unsigned threads)
+{
+    const uint32_t B0 = Node.FaceBeginIndex, E0 = Node.FaceEndIndex;
+    uint32_t FaceCount = E0 - B0;
+    unsigned parts = FaceCount >= BVH_PARALLEL_PASS_FACES ? std::max(1u, threads) : 1u;
+
+    {
+        std::vector<bounds> part(parts);
+        ForChunks(B0, E0, parts, [&](unsigned c, uint32_t b, uint32_t e) {
+            bounds Bd;
+            for (uint32_t Index = b; Index < e; Index++)
+                for (int J = 0; J < 3; J++) Grow(Bd, (*C.V)[(*C.F)[Index].VertexIndex[J]].Position);
+            part[c] = Bd;
+        });
+        Node.Bounds = {};
+        for (auto& Bd : part) Grow(Node.Bounds, Bd);
+    }
 
     int SplitAxis = 0;
     float SplitPosition = 0;
     float SplitCost = +INF;
 
     for (int Axis = 0; Axis < 3; Axis++) {
+        std::vector<float> pmin(parts, +INF), pmax(parts, -INF);
+        ForChunks(B0, E0, parts, [&](unsigned c, uint32_t b, uint32_t e) {
+            float Mn = +INF, Mx = -INF;
+            for (uint32_t FaceIndex = b; FaceIndex < e; FaceIndex++) {
+                float Centroid = FaceCentroid(C, FaceIndex, Axis);
+                Mn = std::min(Mn, Centroid);
+                Mx = std::max(Mx, Centroid);
+            }
+            pmin[c] = Mn;
+            pmax[c] = Mx;
+        });
         float Minimum = +INF, Maximum = -INF;
-        for (uint32_t FaceIndex = Node.FaceBeginIndex; FaceIndex < Node.FaceEndIndex; FaceIndex++) {
-            float Centroid = GetMeshFaceCentroid(Mesh, FaceIndex, Axis);
-            Minimum = std::min(Minimum, Centroid);
-            Maximum = std::max(Maximum, Centroid);
-        }
+        for (unsigned c = 0; c < parts; c++) { Minimum = std::min(Minimum, pmin[c]); Maximum = std::max(Maximum, pmax[c]); }
         if (Minimum == Maximum) continue;
 
-        constexpr uint32_t BINS = 32;
-        struct bin { bounds Bounds; uint32_t FaceCount = 0; };
-        bin Bins[BINS];
-
-        float BinIndexPerUnit = float(BINS) / (Maximum - Minimum);
-        for (uint32_t I = Node.FaceBeginIndex; I < Node.FaceEndIndex; I++) {
-            float Centroid = GetMeshFaceCentroid(Mesh, I, Axis);
-            uint32_t BinIndexUnclamped = static_cast<uint32_t>(BinIndexPerUnit * (Centroid - Minimum));
-            uint32_t BinIndex = std::min(BinIndexUnclamped, BINS - 1);
-            bin& Bin = Bins[BinIndex];
-            Grow(Bin.Bounds, Mesh->Vertices[Mesh->Faces[I].VertexIndex[0]].Position);
-            Grow(Bin.Bounds, Mesh->Vertices[Mesh->Faces[I].VertexIndex[1]].Position);
-            Grow(Bin.Bounds, Mesh->Vertices[Mesh->Faces[I].VertexIndex[2]].Position);
-            Bin.FaceCount++;
-        }
+        float BinIndexPerUnit = float(BVH_BINS) / (Maximum - Minimum);
+        std::vector<std::array<bvh_bin, BVH_BINS>> pbins(parts);
+        ForChunks(B0, E0, parts, [&](unsigned c, uint32_t b, uint32_t e) {
+            auto& Bins = pbins[c];
+            for (uint32_t I = b; I < e; I++) {
+                float Centroid = FaceCentroid(C, I, Axis);
+                uint32_t BinIndexUnclamped = static_cast<uint32_t>(BinIndexPerUnit * (Centroid - Minimum));
+                bvh_bin& Bin = Bins[std::min(BinIndexUnclamped, BVH_BINS - 1)];
+                for (int J = 0; J < 3; J++) Grow(Bin.Bounds, (*C.V)[(*C.F)[I].VertexIndex[J]].Position);
+                Bin.FaceCount++;
+            }
+        });
+        std::array<bvh_bin, BVH_BINS> Bins;
+        for (unsigned c = 0; c < parts; c++)
+            for (uint32_t k = 0; k < BVH_BINS; k++) {
+                Grow(Bins[k].Bounds, pbins[c][k].Bounds);
+                Bins[k].FaceCount += pbins[c][k].FaceCount;
+            }
 
         struct split { float LeftArea = 0; uint32_t LeftCount = 0; float RightArea = 0; uint32_t RightCount = 0; };
-        split Splits[BINS - 1];
+        split Splits[BVH_BINS - 1];
         bounds LeftBounds, RightBounds;
         uint32_t LeftCountSum = 0, RightCountSum = 0;
-        for (uint32_t I = 0; I < BINS - 1; I++) {
-            uint32_t J = BINS - 2 - I;
-            bin const& LeftBin = Bins[I];
+        for (uint32_t I = 0; I < BVH_BINS - 1; I++) {
+            uint32_t J = BVH_BINS - 2 - I;
+            bvh_bin const& LeftBin = Bins[I];
             if (LeftBin.FaceCount > 0) { LeftCountSum += LeftBin.FaceCount; Grow(LeftBounds, LeftBin.Bounds); }
             Splits[I].LeftCount = LeftCountSum;
             Splits[I].LeftArea = HalfArea(LeftBounds);
-            bin const& RightBin = Bins[J + 1];
+            bvh_bin const& RightBin = Bins[J + 1];
             if (RightBin.FaceCount > 0) { RightCountSum += RightBin.FaceCount; Grow(RightBounds, RightBin.Bounds); }
             Splits[J].RightCount = RightCountSum;
             Splits[J].RightArea = HalfArea(RightBounds);
         }
 
-        float Interval = (Maximum - Minimum) / float(BINS);
+        float Interval = (Maximum - Minimum) / float(BVH_BINS);
         float Position = Minimum + Interval;
-        for (uint32_t I = 0; I < BINS - 1; I++) {
+        for (uint32_t I = 0; I < BVH_BINS - 1; I++) {
             split const& Split = Splits[I];
             float Cost = Split.LeftCount * Split.LeftArea + Split.RightCount * Split.RightArea;
             if (Cost < SplitCost) { SplitCost = Cost; SplitAxis = Axis; SplitPosition = Position; }
@@ -132,34 +193,85 @@ void BuildMeshNode(mesh* Mesh, uint32_t NodeIndex, uint32_t Depth)
     }
 
     float NoSplitCost = FaceCount * HalfArea(Node.Bounds);
-    if (SplitCost >= NoSplitCost) return;
+    if (SplitCost >= NoSplitCost) return 0;
 
     // Partition (scene.cpp:556-573); the element where the two indices meet
     // is not examined and ends up on the right.
-    uint32_t BeginIndex = Node.FaceBeginIndex;
-    uint32_t EndIndex = Node.FaceEndIndex;
-    uint32_t SplitIndex = BeginIndex;
-    uint32_t SwapIndex = EndIndex - 1;
+    uint32_t SplitIndex = B0;
+    uint32_t SwapIndex = E0 - 1;
     while (SplitIndex < SwapIndex) {
-        float Centroid = GetMeshFaceCentroid(Mesh, SplitIndex, SplitAxis);
+        float Centroid = FaceCentroid(C, SplitIndex, SplitAxis);
         if (Centroid < SplitPosition) SplitIndex++;
-        else { std::swap(Mesh->Faces[SplitIndex], Mesh->Faces[SwapIndex]); SwapIndex--; }
+        else { std::swap((*C.F)[SplitIndex], (*C.F)[SwapIndex]); SwapIndex--; }
     }
-    if (SplitIndex == BeginIndex || SplitIndex == EndIndex) return;
+    if (SplitIndex == B0 || SplitIndex == E0) return 0;
+    return SplitIndex;
+}
 
-    uint32_t LeftNodeIndex = static_cast<uint32_t>(Mesh->Nodes.size());
+// The reference's recursion over Nodes (children pushed adjacently, then
+// the left subtree, then the right one).
+void BuildMeshNode(const bvh_ctx& C, std::vector<mesh_node>& Nodes, uint32_t& MaxDepth, uint32_t NodeIndex,
+                   uint32_t Depth)
+{
+    uint32_t SplitIndex = SplitMeshNode(C, Nodes[NodeIndex], 1);
+    if (!SplitIndex) return;
+    uint32_t LeftNodeIndex = static_cast<uint32_t>(Nodes.size());
     uint32_t RightNodeIndex = LeftNodeIndex + 1;
-    Node.ChildNodeIndex = LeftNodeIndex;
-
+    Nodes[NodeIndex].ChildNodeIndex = LeftNodeIndex;
     mesh_node Left, Right;
-    Left.FaceBeginIndex = BeginIndex; Left.FaceEndIndex = SplitIndex;
-    Right.FaceBeginIndex = SplitIndex; Right.FaceEndIndex = EndIndex;
-    Mesh->Nodes.push_back(Left);
-    Mesh->Nodes.push_back(Right);
-    Mesh->Depth = std::max(Mesh->Depth, Depth + 1);
+    Left.FaceBeginIndex = Nodes[NodeIndex].FaceBeginIndex; Left.FaceEndIndex = SplitIndex;
+    Right.FaceBeginIndex = SplitIndex; Right.FaceEndIndex = Nodes[NodeIndex].FaceEndIndex;
+    Nodes.push_back(Left);
+    Nodes.push_back(Right);
+    MaxDepth = std::max(MaxDepth, Depth + 1);
+    BuildMeshNode(C, Nodes, MaxDepth, LeftNodeIndex, Depth + 1);
+    BuildMeshNode(C, Nodes, MaxDepth, RightNodeIndex, Depth + 1);
+}
 
-    BuildMeshNode(Mesh, LeftNodeIndex, Depth + 1);
-    BuildMeshNode(Mesh, RightNodeIndex, Depth + 1);
+// Subtree of `Root` as [Root] + its descendants in the reference's order,
+// child indices local to the returned array.  With threads > 1 the two
+// children are built concurrently (threads split between them); their
+// arrays are then spliced: S(X) = [X, L, R] + S(L)[1:] + S(R)[1:].
+std::vector<mesh_node> BuildMeshSubtree(const bvh_ctx& C, mesh_node Root, uint32_t Depth, uint32_t& MaxDepth,
+                                        unsigned threads)
+{
+    std::vector<mesh_node> Out;
+    if (threads <= 1 || Root.FaceEndIndex - Root.FaceBeginIndex < BVH_PARALLEL_PASS_FACES / 4) {
+        Out.reserve(2 * (size_t)(Root.FaceEndIndex - Root.FaceBeginIndex));
+        Out.push_back(Root);
+        BuildMeshNode(C, Out, MaxDepth, 0, Depth);
+        return Out;
+    }
+    uint32_t SplitIndex = SplitMeshNode(C, Root, threads);
+    if (!SplitIndex) { Out.push_back(Root); return Out; }
+    mesh_node Left, Right;
+    Left.FaceBeginIndex = Root.FaceBeginIndex; Left.FaceEndIndex = SplitIndex;
+    Right.FaceBeginIndex = SplitIndex; Right.FaceEndIndex = Root.FaceEndIndex;
+    MaxDepth = std::max(MaxDepth, Depth + 1);
+    uint32_t DL = 0, DR = 0;
+    std::vector<mesh_node> SL, SR;
+    unsigned tl = threads / 2, tr = threads - tl;
+    std::thread worker([&] { SL = BuildMeshSubtree(C, Left, Depth + 1, DL, tl); });
+    SR = BuildMeshSubtree(C, Right, Depth + 1, DR, tr);
+    worker.join();
+    MaxDepth = std::max(MaxDepth, std::max(DL, DR));
+    const uint32_t offL = 2, offR = 2 + (uint32_t)(SL.size() - 1);
+    Out.reserve(1 + SL.size() + SR.size());
+    Root.ChildNodeIndex = 1;
+    Out.push_back(Root);
+    Out.push_back(SL[0]);
+    Out.push_back(SR[0]);
+    if (Out[1].ChildNodeIndex) Out[1].ChildNodeIndex += offL;
+    if (Out[2].ChildNodeIndex) Out[2].ChildNodeIndex += offR;
+    for (size_t i = 1; i < SL.size(); i++) {
+        Out.push_back(SL[i]);
+        if (Out.back().ChildNodeIndex) Out.back().ChildNodeIndex += offL;
+    }
+    for (size_t i = 1; i < SR.size(); i++) {
+        Out.push_back(SR[i]);
+        if (Out.back().ChildNodeIndex) Out.back().ChildNodeIndex += offR;
+    }
+    return Out;
 }
 
 // ShapeBounds (scene.cpp:1031-1093)
@@ -349,17 +461,25 @@ texture* CreateTexture(scene* Scene, const char* Name, uint32_t Type, uint32_t W
     return T;
 }
 
+// Threads for a mesh build: PT_BVH_THREADS, else OMP_NUM_THREADS, else the
+// hardware's; 1 runs the reference's sequential recursion.
+unsigned BvhThreads()
+{
+    unsigned t = std::thread::hardware_concurrency();
+    if (const char* e = std::getenv("OMP_NUM_THREADS")) t = (unsigned)std::max(1, atoi(e));
+    if (const char* e = std::getenv("PT_BVH_THREADS")) t = (unsigned)std::max(1, atoi(e));
+    return std::min(std::max(t, 1u), 64u);
+}
+
 void BuildMeshBVH(mesh* Mesh)   // scene.cpp:851-866
 {
-    Mesh->Nodes.clear();
-    Mesh->Nodes.reserve(2 * Mesh->Faces.size());
     mesh_node Root;
     Root.FaceBeginIndex = 0;
     Root.FaceEndIndex = static_cast<uint32_t>(Mesh->Faces.size());
     Root.ChildNodeIndex = 0;
-    Mesh->Nodes.push_back(Root);
+    bvh_ctx C{&Mesh->Vertices, &Mesh->Faces};
     Mesh->Depth = 0;
-    BuildMeshNode(Mesh, 0, 0);
+    Mesh->Nodes = BuildMeshSubtree(C, Root, 0, Mesh->Depth, BvhThreads());
 }
 
 mesh* CreateMesh(scene* Scene, const char* Name, uint32_t VertexCount, const float* Positions,
