@@ -20,7 +20,7 @@ from test_gpu_parity import compare_hits, compare_state, random_rays, render_pai
 
 pytestmark = pytest.mark.gpu
 
-SEEDS = list(range(12))
+SEEDS = list(range(24))
 
 
 @pytest.fixture(scope="module")
