@@ -169,7 +169,10 @@ def main():
     info = scene.info
     width, height = info.width, info.height
 
-    dev = pt.Device(0 if args.one_gpu_flow_check else local_rank)
+    # One GPU per rank: LOCAL_RANK indexes the visible devices; a launcher
+    # that leaves each rank a single visible device gets device 0.
+    ndev = max(pt.device_count(), 1)
+    dev = pt.Device(0 if args.one_gpu_flow_check else local_rank % ndev)
     dscene = pt.DeviceScene(dev)
     dscene.update(scene)
     sb = pt.SampleBuffer(dev, width, height)
