@@ -432,3 +432,36 @@ def test_edge_scenes_bit_exact(pt, dev, kind, W, H):
     compare_hits(ds.trace_rays(o, v, d), oracle_lib.trace_rays(s.packs(), o, v, d))
     ds.close()
     s.close()
+
+
+def test_large_mesh_bit_exact(pt, dev):
+    """A mesh past the compact forms' limits: 740k unconnected triangles =
+    2.22 M vertices (> 2^21, so hit records carry the face index instead of
+    packed vertex indices) and ~1.5 M BLAS nodes (child-pair indices beyond
+    16 bits, so the traversal stack holds packed 32-bit entries, not u16),
+    under a TLAS with analytic shapes; state, image and random-ray hits
+    bit-exact against the oracle."""
+    import fuzz_scenes
+    rng = np.random.default_rng(17)
+    pos, idx, nrm, uv = fuzz_scenes.soup_mesh(rng, 740000, 2.5)
+    assert len(pos) > (1 << 21)
+    s = pt.Scene.empty()
+    m = s.create_mesh(pos, idx, nrm, uv, name="BigSoup")
+    e = s.create_entity(pt.ENTITY_MESH_INSTANCE, position=(0.0, 0.0, 1.5))
+    s.set_mesh(e, m)
+    s.create_entity(pt.ENTITY_PLANE, position=(0.0, 0.0, -1.0))
+    s.create_entity(pt.ENTITY_SPHERE, position=(2.0, -3.0, 0.5), scale=(0.7, 0.7, 0.7))
+    s.create_entity(pt.ENTITY_CAMERA, position=(0.0, -8.0, 1.5), rotation=(1.57, 0.0, 0.0))
+    s.set_root(skybox_brightness=1.5)
+    s.pack()
+    a = s.arrays()
+    assert len(a["mesh_nodes"]) > (1 << 16)
+    gs, os_, ga, oa = render_pair(pt, dev, None, 80, 48, [2, 1, 1], scene=s)
+    compare_state(gs, os_)
+    assert np.array_equal(bits(ga), bits(oa))
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    o, v, d = random_rays(a, 8192, seed=23)
+    compare_hits(ds.trace_rays(o, v, d), oracle_lib.trace_rays(s.packs(), o, v, d))
+    ds.close()
+    s.close()
