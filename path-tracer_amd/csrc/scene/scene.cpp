@@ -99,8 +99,14 @@ void ForChunks(uint32_t b, uint32_t e, unsigned parts, Body body)
     if (parts <= 1) { body(0u, b, e); return; }
     std::vector<std::thread> pool;
     uint64_t n = e - b;
-    for (unsigned c = 1; c < parts; c++)
-        pool.emplace_back(body, c, (uint32_t)(b + n * c / parts), (uint32_t)(b + n * (c + 1) / parts));
+    for (unsigned c = 1; c < parts; c++) {
+        uint32_t cb = (uint32_t)(b + n * c / parts), ce = (uint32_t)(b + n * (c + 1) / parts);
+        try {
+            pool.emplace_back(body, c, cb, ce);
+        } catch (...) {   // no thread available: this chunk on the calling thread (same result)
+            body(c, cb, ce);
+        }
+    }
     body(0u, b, (uint32_t)(b + n / parts));
     for (auto& t : pool) t.join();
 }
@@ -251,9 +257,14 @@ std::vector<mesh_node> BuildMeshSubtree(const bvh_ctx& C, mesh_node Root, uint32
     uint32_t DL = 0, DR = 0;
     std::vector<mesh_node> SL, SR;
     unsigned tl = threads / 2, tr = threads - tl;
-    std::thread worker([&] { SL = BuildMeshSubtree(C, Left, Depth + 1, DL, tl); });
+    std::thread worker;
+    try {
+        worker = std::thread([&] { SL = BuildMeshSubtree(C, Left, Depth + 1, DL, tl); });
+    } catch (...) {   // no thread available: build the left subtree here first (same result)
+        SL = BuildMeshSubtree(C, Left, Depth + 1, DL, 1);
+    }
     SR = BuildMeshSubtree(C, Right, Depth + 1, DR, tr);
-    worker.join();
+    if (worker.joinable()) worker.join();
     MaxDepth = std::max(MaxDepth, std::max(DL, DR));
     const uint32_t offL = 2, offR = 2 + (uint32_t)(SL.size() - 1);
     Out.reserve(1 + SL.size() + SR.size());
