@@ -465,3 +465,69 @@ def test_large_mesh_bit_exact(pt, dev):
     compare_hits(ds.trace_rays(o, v, d), oracle_lib.trace_rays(s.packs(), o, v, d))
     ds.close()
     s.close()
+
+
+def test_editor_updates_bit_exact(pt, dev):
+    """The editor's other edits, each followed by PackSceneData's dirty flags,
+    a partial ptUpdateScene with them, and Reset + Run(2) + Run(1) on the same
+    renderer (application.cpp:100-115, scene.hpp:323-333): a material
+    parameter, an entity transform (TLAS rebuild), a new deeper mesh instance
+    (meshes + shapes; the traversal stack bound grows), the sky.  Each state
+    is bit-exact against a fresh oracle on the updated packs."""
+    import fuzz_scenes
+    rng = np.random.default_rng(29)
+    s = pt.Scene.empty()
+    red = s.create_material(pt.MATERIAL_BASIC_DIFFUSE, "Red", BaseColor=(0.8, 0.2, 0.2))
+    metal = s.create_material(pt.MATERIAL_BASIC_METAL, "Metal", BaseColor=(0.9, 0.8, 0.5), Roughness=0.2)
+    glass = s.create_material(pt.MATERIAL_BASIC_TRANSLUCENT, "Glass", IOR=1.5, Roughness=0.0)
+    s.create_entity(pt.ENTITY_PLANE, material=red)
+    ball = s.create_entity(pt.ENTITY_SPHERE, position=(0.0, 0.0, 1.0), material=glass)
+    s.create_entity(pt.ENTITY_CUBE, position=(1.5, 1.0, 0.5), scale=(0.5, 0.5, 0.5), material=metal)
+    blob = s.create_mesh(*fuzz_scenes.blob_mesh(rng, 6, 10, 0.1))
+    e = s.create_entity(pt.ENTITY_MESH_INSTANCE, position=(-1.5, 0.5, 0.8), scale=(0.6, 0.6, 0.6), material=metal)
+    s.set_mesh(e, blob)
+    s.create_entity(pt.ENTITY_CAMERA, position=(0.0, -5.0, 1.5), rotation=(1.4, 0.0, 0.0))
+    s.set_root(skybox_brightness=1.0)
+    s.pack()
+    W, H = 96, 64
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    sb = pt.SampleBuffer(dev, W, H)
+    r = pt.BasicRenderer(dev, ds, sb)
+    r.RenderFlags = 3
+
+    def render_and_check():
+        frame = r.FrameIndex
+        r.reset()
+        r.run(2)
+        r.run(1)
+        o = oracle_lib.OracleRenderer(s.packs(), W, H)
+        o.RenderFlags = 3
+        o.FrameIndex = frame
+        o.reset()
+        o.run(2)
+        o.run(1)
+        dev.synchronize()
+        compare_state(r.read_state(), o.state())
+        assert np.array_equal(bits(sb.read()), bits(o.accum()))
+        o.close()
+
+    render_and_check()
+    edits = [
+        lambda: s.set_material_parameter(red, "BaseColor", (0.2, 0.7, 0.3)),
+        lambda: s.set_transform(ball, position=(0.4, 0.3, 1.2), rotation=(0.0, 0.3, 0.0), scale=(0.8, 1.0, 1.2)),
+        lambda: s.set_mesh(s.create_entity(pt.ENTITY_MESH_INSTANCE, position=(0.0, 1.5, 0.6), material=red),
+                           s.create_mesh(*fuzz_scenes.soup_mesh(rng, 3000, 0.6))),
+        lambda: s.set_root(skybox_brightness=2.5, scatter_rate=0.02),
+    ]
+    stack0 = ds.stack_needed
+    for edit in edits:
+        edit()
+        dirty = s.pack()
+        assert dirty != 0
+        ds.update(s, dirty)
+        render_and_check()
+    assert ds.stack_needed > stack0        # the soup's BVH is deeper than the blob's
+    for x in (r, sb, ds):
+        x.close()
+    s.close()
