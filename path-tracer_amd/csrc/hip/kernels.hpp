@@ -79,8 +79,12 @@ enum : uint32_t {
     PT_MATS_OPENPBR = 16,     // OpenPBR shapes shaded (ptSetBasicRendererOpenPBR); instantiated as ALL | OPENPBR
 };
 uint32_t pt_shade_mats(uint32_t scene_mats);
+// Preview base-colour tables: the 16 sample constants of ObserveUnderD65
+// (preview.hip), filled once per preview context.
+constexpr uint32_t PT_OBSERVE_TABLE_FLOATS = 16 * 5;
+hipError_t pt_launch_observe_table(float* table, hipStream_t st);
 hipError_t pt_launch_preview(const ptd::dscene& S, const pt_preview_parameters* p, uint32_t* spill, float4* out,
-                             pt_preview_aov* aov, uint32_t* query, hipStream_t st);
+                             pt_preview_aov* aov, uint32_t* query, const float* observe_table, hipStream_t st);
 uint32_t pt_preview_stack_cap();
 hipError_t pt_launch_resolve(const float4* accum, uint32_t n, float brightness, uint32_t mode, float white, float4* out,
                              uint32_t* out8, hipStream_t st);

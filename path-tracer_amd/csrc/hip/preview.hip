@@ -33,38 +33,58 @@ PT_DEV float SampleIlluminantD65(float NormalizedLambda)              // spectru
 }
 
 // ObserveParametricSpectrumUnderD65 (spectrum.glsl.inc:194-208), 16 samples.
-PT_DEV pt3 ObserveUnderD65(pt4 BetaAndIntensity)
+// Everything but the spectrum itself -- each sample's wavelength, D65 weight
+// and CIE observer value -- depends on the sample index only, so
+// observe_table_kernel evaluates the 16 samples once per preview context and
+// every observation reads them (uniform index: scalar loads): the same
+// functions on the same operands give the same bits, and the 7 exponentials
+// of each observer value leave the per-pixel path.
+constexpr int OBSERVE_SAMPLES = 16;
+struct observe_table {
+    float D[OBSERVE_SAMPLES], Lambda[OBSERVE_SAMPLES];
+    pt3 Obs[OBSERVE_SAMPLES];
+};
+
+static_assert(sizeof(observe_table) == PT_OBSERVE_TABLE_FLOATS * 4, "observe_table size");
+
+__global__ void observe_table_kernel(observe_table* T)
 {
-    const int SampleCount = 16;
-    const float DeltaLambda = (PT_CIE_LAMBDA_MAX - PT_CIE_LAMBDA_MIN) / SampleCount;
+    const int I = (int)threadIdx.x;
+    if (I >= OBSERVE_SAMPLES) return;
+    float NormalizedLambda = (float)I / (float)(OBSERVE_SAMPLES - 1);
+    T->D[I] = SampleIlluminantD65(NormalizedLambda) / PT_CIE_D65_NORMALIZATION;
+    T->Lambda[I] = pt_mix(PT_CIE_LAMBDA_MIN, PT_CIE_LAMBDA_MAX, NormalizedLambda);
+    T->Obs[I] = SampleStandardObserver(T->Lambda[I]);
+}
+
+PT_DEV pt3 ObserveUnderD65(const observe_table& T, pt4 BetaAndIntensity)
+{
+    const float DeltaLambda = (PT_CIE_LAMBDA_MAX - PT_CIE_LAMBDA_MIN) / OBSERVE_SAMPLES;
     pt3 Color = v3s(0);
     pt3 Beta = v3(BetaAndIntensity.x, BetaAndIntensity.y, BetaAndIntensity.z);
-    for (int I = 0; I < SampleCount; I++) {
-        float NormalizedLambda = (float)I / (float)(SampleCount - 1);
-        float D = SampleIlluminantD65(NormalizedLambda) / PT_CIE_D65_NORMALIZATION;
-        float Lambda = pt_mix(PT_CIE_LAMBDA_MIN, PT_CIE_LAMBDA_MAX, NormalizedLambda);
-        float Sp = BetaAndIntensity.w * SampleParametricSpectrum(Beta, Lambda);
-        Color = Color + Sp * D * SampleStandardObserver(Lambda) * DeltaLambda;
+    for (int I = 0; I < OBSERVE_SAMPLES; I++) {
+        float Sp = BetaAndIntensity.w * SampleParametricSpectrum(Beta, T.Lambda[I]);
+        Color = Color + Sp * T.D[I] * T.Obs[I] * DeltaLambda;
     }
     return Color;
 }
 
-PT_DEV pt3 ObserveUnderD65(pt3 Beta) { return ObserveUnderD65(v4(Beta.x, Beta.y, Beta.z, 1)); }
+PT_DEV pt3 ObserveUnderD65(const observe_table& T, pt3 Beta) { return ObserveUnderD65(T, v4(Beta.x, Beta.y, Beta.z, 1)); }
 
 // MaterialBaseColor (scene.glsl.inc:254-274,696-701 + *_BaseColor)
-PT_DEV pt3 MaterialBaseColor(const dscene& S, uint32_t M, pt2 UV)
+PT_DEV pt3 MaterialBaseColor(const dscene& S, const observe_table& Tb, uint32_t M, pt2 UV)
 {
     uint32_t Type = MUint(S, M, 0);
     uint32_t A;
     if (Type == PT_MATERIAL_TYPE_BASIC_DIFFUSE) A = PT_BASIC_DIFFUSE_BASE_SPECTRUM;
     else if (Type == PT_MATERIAL_TYPE_BASIC_METAL) A = PT_BASIC_METAL_BASE_SPECTRUM;
-    else if (Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT) return ObserveUnderD65(MVec3(S, M, PT_BASIC_TRANSLUCENT_TRANSMISSION_SPECTRUM));
+    else if (Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT) return ObserveUnderD65(Tb, MVec3(S, M, PT_BASIC_TRANSLUCENT_TRANSMISSION_SPECTRUM));
     else return v3s(0);
-    pt3 Color = ObserveUnderD65(MVec3(S, M, A));
+    pt3 Color = ObserveUnderD65(Tb, MVec3(S, M, A));
     uint32_t TextureIndex = MUint(S, M, A + 3);
     if (TextureIndex != TEXTURE_INDEX_NONE) {
         pt4 T = SampleTexture(S, TextureIndex, UV);
-        Color = Color * ObserveUnderD65(v3(T.x, T.y, T.z));
+        Color = Color * ObserveUnderD65(Tb, v3(T.x, T.y, T.z));
     }
     return Color;
 }
@@ -114,9 +134,11 @@ struct ray_source_preview {
 template <int CAP>
 __global__ __launch_bounds__(256) void preview_kernel(dscene S, preview_args P, uint32_t* spill, uint32_t spill_stride,
                                                       float4* __restrict__ out, pt_preview_aov* __restrict__ aov,
-                                                      uint32_t* __restrict__ query)
+                                                      uint32_t* __restrict__ query,
+                                                      const observe_table* __restrict__ observe)
 {
     __shared__ uint32_t smem[CAP * 256];
+    const observe_table& Tb = *observe;
     uint32_t i = blockIdx.x * 256 + threadIdx.x;
     ray_source_preview src{&P};
     uint32_t x, y;
@@ -146,9 +168,9 @@ __global__ __launch_bounds__(256) void preview_kernel(dscene S, preview_args P, 
     case PT_PREVIEW_RENDER_MODE_BASE_COLOR:
     case PT_PREVIEW_RENDER_MODE_BASE_COLOR_SHADED:
         if (Miss) {
-            Color = XYZToSRGB(ObserveUnderD65(SampleSkyboxSpectrum(S, V)));
+            Color = XYZToSRGB(ObserveUnderD65(Tb, SampleSkyboxSpectrum(S, V)));
         } else {
-            Color = XYZToSRGB(MaterialBaseColor(S, Material, UV));
+            Color = XYZToSRGB(MaterialBaseColor(S, Tb, Material, UV));
             if (P.mode == PT_PREVIEW_RENDER_MODE_BASE_COLOR_SHADED) Color = Color * dot(N, -V);
         }
         break;
@@ -189,8 +211,15 @@ __global__ __launch_bounds__(256) void preview_kernel(dscene S, preview_args P, 
 
 }  // namespace ptd
 
+hipError_t pt_launch_observe_table(float* table, hipStream_t st)
+{
+    hipLaunchKernelGGL(ptd::observe_table_kernel, dim3(1), dim3(64), 0, st,
+                       reinterpret_cast<ptd::observe_table*>(table));
+    return hipGetLastError();
+}
+
 hipError_t pt_launch_preview(const ptd::dscene& S, const pt_preview_parameters* p, uint32_t* spill, float4* out,
-                             pt_preview_aov* aov, uint32_t* query, hipStream_t st)
+                             pt_preview_aov* aov, uint32_t* query, const float* observe_table, hipStream_t st)
 {
     ptd::preview_args P;
     P.cam = p->CameraTransform;
@@ -204,7 +233,8 @@ hipError_t pt_launch_preview(const ptd::dscene& S, const pt_preview_parameters* 
     P.tiles_x = (P.w + 15) / 16;
     uint32_t tiles = P.tiles_x * ((P.h + 15) / 16);
     if (tiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(ptd::preview_kernel<20>, dim3(tiles), dim3(256), 0, st, S, P, spill, tiles * 256, out, aov, query);
+    hipLaunchKernelGGL(ptd::preview_kernel<20>, dim3(tiles), dim3(256), 0, st, S, P, spill, tiles * 256, out, aov, query,
+                       reinterpret_cast<const ptd::observe_table*>(observe_table));
     return hipGetLastError();
 }
 

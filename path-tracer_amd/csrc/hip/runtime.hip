@@ -127,6 +127,7 @@ struct pt_preview {
     dbuf<float4> image;
     dbuf<pt_preview_aov> aov;
     dbuf<uint32_t> spill;
+    dbuf<float> observe;                 // ObserveUnderD65's per-sample constants (preview.hip)
     uint32_t* query = nullptr;
     bool rendered = false;
 };
@@ -1033,6 +1034,13 @@ pt_preview* ptCreatePreviewRenderContext(pt_device* d, pt_scene* s)
         delete c;
         return nullptr;
     }
+    if (c->observe.alloc(PT_OBSERVE_TABLE_FLOATS) != hipSuccess || pt_launch_observe_table(c->observe.ptr, d->stream) != hipSuccess) {
+        SetError("preview table set-up failed");
+        c->observe.release();
+        (void)hipFree(c->query);
+        delete c;
+        return nullptr;
+    }
     return c;
 }
 
@@ -1043,6 +1051,7 @@ void ptDestroyPreviewRenderContext(pt_device* d, pt_preview* c)
     c->image.release();
     c->aov.release();
     c->spill.release();
+    c->observe.release();
     if (c->query) (void)hipFree(c->query);
     delete c;
 }
@@ -1070,7 +1079,7 @@ int ptRenderPreview(pt_device* d, pt_preview* c, const pt_preview_parameters* p)
     }
     event_pair ep{};
     if (int e = BeginTimed(d, PT_KERNEL_PREVIEW, ep)) return e;
-    PT_HIP(pt_launch_preview(c->scene->d, p, spill, c->image.ptr, c->aov.ptr, c->query, d->stream));
+    PT_HIP(pt_launch_preview(c->scene->d, p, spill, c->image.ptr, c->aov.ptr, c->query, c->observe.ptr, d->stream));
     if (int e = EndTimed(d, ep)) return e;
     c->width = p->RenderSizeX;
     c->height = p->RenderSizeY;
