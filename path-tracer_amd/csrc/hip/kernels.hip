@@ -1159,10 +1159,12 @@ __global__ __launch_bounds__(256) void finalize_kernel(dscene S, uint32_t n, con
 #ifndef PT_SHADE_OTHER_MINW
 #define PT_SHADE_OTHER_MINW 5
 #endif
-// The OpenPBR instantiation (opt-in) carries the layered sampler as well: no
-// occupancy floor beyond the launch's own, so its registers are not spilled.
+// The OpenPBR instantiation (opt-in) carries the layered sampler as well:
+// 160 VGPRs (3 waves/SIMD) unbounded; a 4-wave floor caps it at 128 with
+// 84 B of spills and is faster (OpenPBR test scene at 1080p: shade 0.523 vs
+// 0.568 ms, profiles/r02_next).
 #ifndef PT_SHADE_OPENPBR_MINW
-#define PT_SHADE_OPENPBR_MINW 1
+#define PT_SHADE_OPENPBR_MINW 4
 #endif
 template <uint32_t MATS>
 constexpr int ShadeMinWaves()
