@@ -1050,6 +1050,19 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, 
     for (uint32_t t = threadIdx.x; t < tiles; t += 1024) order[atomicAdd(&count[key(t)], 1u)] = base + t;
 }
 
+// Mesh vertices decoded once per upload for HitAttributes: the octahedral
+// normal (UnpackUnitVector) and the half-float UV, the functions the hit
+// reconstruction applied per hit before, so every hit sees the same bits.
+__global__ __launch_bounds__(256) void vertex_decode_kernel(const uint2* v, uint32_t n, float4* attr, float* vv)
+{
+    uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint2 V = v[i];
+    pt3 N = UnpackUnitVector(V.x);
+    attr[i] = make_float4(N.x, N.y, N.z, pt_half_to_float(V.y & 0xFFFF));
+    vv[i] = pt_half_to_float(V.y >> 16);
+}
+
 // Row-major packed atlas -> the device's 4x2-texel block layout (AtlasIndex):
 // one thread per destination texel, so the stores are contiguous.
 __global__ __launch_bounds__(256) void atlas_tile_kernel(const float4* src, float4* dst, uint32_t w, uint32_t h,
@@ -1441,6 +1454,13 @@ hipError_t pt_launch_extend_stats(const ptd::dscene& S, const ptd::dslots& L, co
         PT_EXTEND_VARIANTS(X)
 #undef X
     }
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_vertex_decode(const uint2* v, uint32_t n, float4* attr, float* vv, hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(ptd::vertex_decode_kernel, dim3((n + 255) / 256), dim3(256), 0, st, v, n, attr, vv);
     return hipGetLastError();
 }
 

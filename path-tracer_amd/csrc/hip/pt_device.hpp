@@ -29,6 +29,9 @@ struct dscene {
     const float4* shape_nodes;     // 2 x float4 per node
     const float4* mesh_faces;      // 3 x float4 per face: {Position0, Edge1, Edge2}, .w = vertex indices
     const uint2* mesh_vertices;
+    const float4* vertex_attr;     // per vertex, decoded once at upload (vertex_decode_kernel):
+                                   // {UnpackUnitVector(PackedNormal), U as float}
+    const float* vertex_v;         // per vertex: V as float
     const float4* mesh_nodes;      // 2 x float4 per node
     const pt_packed_camera* cameras;
     const float4* atlas;

@@ -100,6 +100,8 @@ struct pt_scene {
     dbuf<pt_packed_shape_node> shape_nodes;
     dbuf<pt_packed_mesh_face> faces;
     dbuf<pt_packed_mesh_vertex> vertices;
+    dbuf<float4> vertex_attr;            // decoded vertex normals + U (vertex_decode_kernel)
+    dbuf<float> vertex_v;                // decoded V
     dbuf<pt_packed_mesh_node> mesh_nodes;
     dbuf<pt_packed_camera> cameras;
     dbuf<float> atlas;
@@ -441,7 +443,7 @@ void ptDestroyScene(pt_device* d, pt_scene* s)
     if (!s) return;
     if (d) (void)hipSetDevice(d->id);
     s->textures.release(); s->material.release(); s->shapes.release(); s->shape_nodes.release();
-    s->faces.release(); s->vertices.release(); s->mesh_nodes.release(); s->cameras.release(); s->atlas.release();
+    s->faces.release(); s->vertices.release(); s->vertex_attr.release(); s->vertex_v.release(); s->mesh_nodes.release(); s->cameras.release(); s->atlas.release();
     delete s;
 }
 
@@ -552,6 +554,10 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
             }
         PT_HIP(s->faces.upload(ef.data(), ef.size()));
         PT_HIP(s->vertices.upload(p->mesh_vertices, p->mesh_vertex_count));
+        PT_HIP(s->vertex_attr.alloc(std::max<size_t>(p->mesh_vertex_count, 1)));
+        PT_HIP(s->vertex_v.alloc(std::max<size_t>(p->mesh_vertex_count, 1)));
+        PT_HIP(pt_launch_vertex_decode(reinterpret_cast<const uint2*>(s->vertices.ptr), p->mesh_vertex_count,
+                                       s->vertex_attr.ptr, s->vertex_v.ptr, d->stream));
         PT_HIP(s->mesh_nodes.upload(p->mesh_nodes, p->mesh_node_count));
     }
     if (first || (dirty & PT_SCENE_DIRTY_CAMERAS)) PT_HIP(s->cameras.upload(p->cameras, p->camera_count));
@@ -564,6 +570,8 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     D.shape_nodes = reinterpret_cast<const float4*>(s->shape_nodes.ptr);
     D.mesh_faces = reinterpret_cast<const float4*>(s->faces.ptr);
     D.mesh_vertices = reinterpret_cast<const uint2*>(s->vertices.ptr);
+    D.vertex_attr = s->vertex_attr.ptr;
+    D.vertex_v = s->vertex_v.ptr;
     D.mesh_nodes = reinterpret_cast<const float4*>(s->mesh_nodes.ptr);
     D.cameras = s->cameras.ptr;
     D.atlas = reinterpret_cast<const float4*>(s->atlas.ptr);

@@ -630,15 +630,18 @@ PT_DEV void HitAttributesV(const dscene& S, uint32_t ShapeIndex, bool packed, ui
             const float4* Fp = S.mesh_faces + 3 * (size_t)Z;   // Z = Prim
             i0 = __float_as_uint(Fp[0].w); i1 = __float_as_uint(Fp[1].w); i2 = __float_as_uint(Fp[2].w);
         }
-        uint2 V0 = S.mesh_vertices[i0];
-        uint2 V1 = S.mesh_vertices[i1];
-        uint2 V2 = S.mesh_vertices[i2];
-        pt3 N = SafeNormalize(UnpackUnitVector(V0.x) * C.x + UnpackUnitVector(V1.x) * C.y + UnpackUnitVector(V2.x) * C.z);
+        // The vertices' normals and UVs come decoded (dscene::vertex_attr:
+        // UnpackUnitVector and the half -> float conversions run once per
+        // vertex at upload, with the same functions, so the same bits).
+        float4 A0 = S.vertex_attr[i0];
+        float4 A1 = S.vertex_attr[i1];
+        float4 A2 = S.vertex_attr[i2];
+        pt3 N = SafeNormalize(xyz(A0) * C.x + xyz(A1) * C.y + xyz(A2) * C.z);
         Normal = TransformNormal(N, From);
         TangentX = ComputeTangentVector(Normal);
-        pt2 UV0 = v2(pt_half_to_float(V0.y & 0xFFFF), pt_half_to_float(V0.y >> 16));
-        pt2 UV1 = v2(pt_half_to_float(V1.y & 0xFFFF), pt_half_to_float(V1.y >> 16));
-        pt2 UV2 = v2(pt_half_to_float(V2.y & 0xFFFF), pt_half_to_float(V2.y >> 16));
+        pt2 UV0 = v2(A0.w, S.vertex_v[i0]);
+        pt2 UV1 = v2(A1.w, S.vertex_v[i1]);
+        pt2 UV2 = v2(A2.w, S.vertex_v[i2]);
         UV = UV0 * C.x + UV1 * C.y + UV2 * C.z;
     } else if (Type == PT_SHAPE_TYPE_PLANE) {
         Normal = TransformNormal(v3(0, 0, 1), From);
