@@ -294,9 +294,19 @@ PT_HD uint32_t pt_pack_snorm16(float v)
     return (uint32_t)(uint16_t)(int16_t)i;
 }
 
+/* glm::unpackSnorm2x16 component: clamp(x / 32767, -1, 1) for the int16 x.
+   The quotient is evaluated as q = RN(x * RN(1/32767)) and one FMA residual
+   correction (Markstein), which equals the IEEE quotient for every one of
+   the 65 536 inputs (checked exhaustively with exact rational arithmetic and
+   against the division, tests/test_numerics.py): 3 operations instead of a
+   division on the device. */
 PT_HD float pt_unpack_snorm16(uint32_t bits)
 {
-    float f = (float)(int16_t)(uint16_t)bits / 32767.0f;
+    const float r = 1.0f / 32767.0f;
+    float x = (float)(int16_t)(uint16_t)bits;
+    float q = x * r;
+    float e = pt_fma(-q, 32767.0f, x);
+    float f = pt_fma(e, r, q);
     return pt_clamp(f, -1.0f, 1.0f);
 }
 

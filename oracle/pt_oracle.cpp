@@ -1751,6 +1751,7 @@ float oracle_fp_atan2(float y, float x) { return pt_atan2(y, x); }
 float oracle_fp_asin(float x) { return pt_asin(x); }
 uint32_t oracle_pcg(uint32_t* state) { return pt_random(state); }
 uint32_t oracle_pack_unit_vector(const float v[3]) { return PackUnitVector(v3(v[0], v[1], v[2])); }
+float oracle_unpack_snorm16(uint32_t bits) { return pt_unpack_snorm16(bits); }
 void oracle_unpack_unit_vector(uint32_t packed, float out[3])
 {
     pt3 v = UnpackUnitVector(packed);

@@ -60,6 +60,7 @@ float oracle_fp_atan2(float y, float x);
 float oracle_fp_asin(float x);
 uint32_t oracle_pcg(uint32_t* state);
 uint32_t oracle_pack_unit_vector(const float v[3]);
+float oracle_unpack_snorm16(uint32_t bits);
 void oracle_unpack_unit_vector(uint32_t packed, float out[3]);
 void oracle_sample_observer(float lambda, float out[3]);
 

@@ -51,6 +51,8 @@ def lib():
         L.oracle_pack_unit_vector.restype = u32
         L.oracle_pack_unit_vector.argtypes = [fptr]
         L.oracle_unpack_unit_vector.argtypes = [u32, fptr]
+        L.oracle_unpack_snorm16.restype = f32
+        L.oracle_unpack_snorm16.argtypes = [u32]
         L.oracle_sample_observer.argtypes = [f32, fptr]
         L.oracle_resolve.argtypes = [fptr, u32, vp, fptr, C.POINTER(C.c_uint8)]
         L.oracle_preview.argtypes = [vp, vp, fptr, vp, C.POINTER(C.c_uint32)]

@@ -136,3 +136,15 @@ def test_transcendentals_golden():
         f = getattr(L, f"oracle_fp_{name}")
         got = np.array([f(float(v)) for v in g[f"{name}_x"]], dtype=np.float32)
         assert np.array_equal(got.view(np.uint32), g[f"{name}_y"].view(np.uint32)), name
+
+
+def test_unpack_snorm16_equals_ieee_quotient_exhaustively():
+    """pt_unpack_snorm16 evaluates x / 32767 as RN(x * RN(1/32767)) plus one
+    FMA residual correction (include/pt_fp.h); for every one of the 65 536
+    int16 inputs it must equal the correctly rounded quotient (numpy float32
+    division), clamped to [-1, 1] as glm::unpackSnorm2x16 does."""
+    L = oracle_lib.lib()
+    x = np.arange(-32768, 32768, dtype=np.int64)
+    want = np.clip(x.astype(np.float32) / np.float32(32767.0), np.float32(-1), np.float32(1)).astype(np.float32)
+    got = np.array([L.oracle_unpack_snorm16(int(v) & 0xFFFF) for v in x], dtype=np.float32)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
