@@ -58,12 +58,23 @@ def build_hip(force=False, verbose=True, out=None, extra=()):
     out = Path(out) if out else HIP_LIB
     if not force and not _stale(out, HIP_SRC + HIP_HDR + [Path(__file__)]):
         return out
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-O3", "-fPIC", "-shared",
-           # -fno-slp-vectorize: no v_pk_* f32 packing (and its operand moves);
-           # shade 0.164 -> 0.156 ms on C3, extend unchanged (tools/gpu_ab.sh).
-           "-ffp-contract=off", "-fno-gpu-rdc", "-munsafe-fp-atomics", "-fno-slp-vectorize",
-           "-Wno-unused-result", *extra, "-o", out] + HIP_SRC + [f"-L{ROCM}/lib", "-lrccl"]
-    _run(cmd, verbose)
+    flags = [f"--offload-arch={ARCH}", "-std=c++17", "-O3", "-fPIC",
+             # -fno-slp-vectorize: no v_pk_* f32 packing (and its operand moves);
+             # shade 0.164 -> 0.156 ms on C3, extend unchanged (tools/gpu_ab.sh).
+             "-ffp-contract=off", "-fno-gpu-rdc", "-munsafe-fp-atomics", "-fno-slp-vectorize",
+             "-Wno-unused-result", *extra]
+    # One object per source, compiled concurrently, then one link.
+    import concurrent.futures
+    import tempfile
+    with tempfile.TemporaryDirectory(prefix="pt_build_") as tmp:
+        objs = [Path(tmp) / (src.stem + ".o") for src in HIP_SRC]
+        with concurrent.futures.ThreadPoolExecutor(max_workers=min(len(HIP_SRC), os.cpu_count() or 1)) as ex:
+            jobs = [ex.submit(_run, [HIPCC, *flags, "-c", str(src), "-o", str(obj)], verbose)
+                    for src, obj in zip(HIP_SRC, objs)]
+            for j in jobs:
+                j.result()
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fno-gpu-rdc", "-o", str(out), *map(str, objs),
+              f"-L{ROCM}/lib", "-lrccl"], verbose)
     return out
 
 
