@@ -489,7 +489,7 @@ PT_DEV bool SampleSurfaceIntegrand(const dscene& S, rng& G, pt3 Nrm, pt3 TX, pt3
     pt3 Mu = v3(dot(SMD, TX), dot(SMD, TY), dot(SMD, Nrm));
     bool ok;
     if (G.R01() < LightProbability) {
-        In = RandomVonMisesFisher(G, S.g.SkyboxConcentration, Mu);
+        In = RandomVonMisesFisher(G, vmf_consts{S.vmf_inv_kappa, S.vmf_exp_m2k, S.vmf_norm}, Mu);
         if (In.z < 0.0f) return false;
         // MaterialEvaluateBSDF(Parameters, Out, In, ...)
         if ((MATS & PT_MATS_DIFFUSE) && Type == PT_MATERIAL_TYPE_BASIC_DIFFUSE)
@@ -517,7 +517,8 @@ PT_DEV bool SampleSurfaceIntegrand(const dscene& S, rng& G, pt3 Nrm, pt3 TX, pt3
         }
         if (!ok) return false;
     }
-    pt4 SkyboxPDF = v4s(VonMisesFisherPDF(S.g.SkyboxConcentration, Mu, In));
+    pt4 SkyboxPDF = v4s(VonMisesFisherPDF(S.g.SkyboxConcentration, vmf_consts{S.vmf_inv_kappa, S.vmf_exp_m2k, S.vmf_norm},
+                                          Mu, In));
     Probability = LightProbability * SkyboxPDF + (1 - LightProbability) * MaterialPDF;
     return true;
 }

@@ -43,6 +43,7 @@ struct dscene {
     uint32_t stack16;              // every stack entry fits 16 bits: extend runs the u16-stack kernel
     uint32_t mat_classes;          // shapes use more than one material type: extend classes hits by type
     uint32_t vidx21;               // every vertex index fits 21 bits: hit records carry a face's vertex indices
+    float vmf_inv_kappa, vmf_exp_m2k, vmf_norm;   // VmfConstants(g.SkyboxConcentration), set on upload
 };
 
 struct ray { pt3 Origin; pt3 Velocity; float Duration; };
@@ -203,10 +204,28 @@ PT_DEV pt3 RandomDirection(rng& G)
     return v3(R * pt_cos(Phi), R * pt_sin(Phi), Z);
 }
 
-PT_DEV pt3 RandomVonMisesFisher(rng& G, float Kappa, pt3 Mu)
+// The sky lobe's Kappa-only factors (common.glsl.inc:222-276), evaluated once
+// per scene upload on the host with the same pt_fp.h functions (IEEE f32, the
+// same FMA polynomials), so the per-hit expressions below see the same bits
+// as the inline ones of the reference restatement.
+struct vmf_consts {
+    float inv_kappa;   // 1 / Kappa
+    float exp_m2k;     // exp(-2 Kappa)
+    float norm;        // Kappa / (2 pi (1 - exp(-2 Kappa)))
+};
+PT_HD vmf_consts VmfConstants(float Kappa)
+{
+    vmf_consts c;
+    c.inv_kappa = 1 / Kappa;
+    c.exp_m2k = pt_exp(-2 * Kappa);
+    c.norm = Kappa / (2 * PT_PI * (1 - pt_exp(-2 * Kappa)));
+    return c;
+}
+
+PT_DEV pt3 RandomVonMisesFisher(rng& G, const vmf_consts& K, pt3 Mu)
 {
     float Xi = G.R01();
-    float Z = 1 + (1 / Kappa) * pt_log(Xi + (1 - Xi) * pt_exp(-2 * Kappa));
+    float Z = 1 + K.inv_kappa * pt_log(Xi + (1 - Xi) * K.exp_m2k);
     float R = pt_sqrt(1 - Z * Z);
     float Phi = G.R01() * PT_TAU;
     pt3 V = v3(R * pt_cos(Phi), R * pt_sin(Phi), Z);
@@ -215,11 +234,10 @@ PT_DEV pt3 RandomVonMisesFisher(rng& G, float Kappa, pt3 Mu)
     return SafeNormalize(V.x * MuX + V.y * MuY + V.z * Mu);
 }
 
-PT_DEV float VonMisesFisherPDF(float Kappa, pt3 Mu, pt3 Direction)
+PT_DEV float VonMisesFisherPDF(float Kappa, const vmf_consts& K, pt3 Mu, pt3 Direction)
 {
     if (Kappa < PT_EPSILON) return 1.0f / (4 * PT_PI);
-    float C = Kappa / (2 * PT_PI * (1 - pt_exp(-2 * Kappa)));
-    return C * pt_exp(Kappa * (dot(Mu, Direction) - 1.0f));
+    return K.norm * pt_exp(Kappa * (dot(Mu, Direction) - 1.0f));
 }
 
 PT_DEV pt3 SampleDirectionHG(float Anisotropy, float U1, float U2)

@@ -564,6 +564,12 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
 
     ptd::dscene& D = s->d;
     D.g = *p->globals;
+    {
+        ptd::vmf_consts K = ptd::VmfConstants(D.g.SkyboxConcentration);
+        D.vmf_inv_kappa = K.inv_kappa;
+        D.vmf_exp_m2k = K.exp_m2k;
+        D.vmf_norm = K.norm;
+    }
     D.textures = s->textures.ptr;
     D.material = s->material.ptr;
     D.shapes = s->shapes.ptr;
