@@ -1,23 +1,31 @@
-"""Benchmark: Mrays/s of the wavefront integrator on the C3 room scene
-(BASELINE.json metric "Mrays/s + Msamples/s, Viking Room 1920x1080 1024spp,
-1/2/4/8 GPUs"; --config 4 for C4, 3840x2160 over 8 GPUs).
+"""Benchmark: Mrays/s of the wavefront integrator over whole frames of the
+BASELINE.json metric "Mrays/s + Msamples/s, Viking Room 1920x1080 1024spp,
+1/2/4/8 GPUs" (C3; --config 4 for C4, 3840x2160 4096spp over 8 GPUs).
 
-A step is one integrator round (extend + shade over every pixel slot, i.e.
-one RunBasicRenderer(1)).  Inputs (scene, slot state) are resident in HBM
-before timing starts.  For N GPUs (one process per GPU, launched by
-torch.distributed.run) the job is sharded one of two ways (--shard):
+A step is one frame in SURVEY.md §8(d)'s benchmark mode: Reset, Run(2), then
+Run(1) rounds until the paths completed since the Reset reach the config's spp
+target x pixels (ptRenderFrame; the application's frame loop,
+application.cpp:100-115, basic.cpp:285-332), plus the frame-end exchange for
+N GPUs.  `value` = rays traced by all ranks / the max over ranks of the timed
+frames' wall time.  Inputs (scene, buffers) are resident in HBM before timing
+starts.
 
-* samples (default, all single-GPU configs): north_star's "pixels/samples
-  shard embarrassingly ... RCCL reduce of the per-pixel radiance and
-  sample-count buffers at frame end".  Every rank renders the whole frame with
-  its own RNG stream (FrameIndex offset rank << 24), so the frame's spp
-  target is split over the ranks; the frame-end ncclReduce of the XYZ sums and
-  sample counts into rank 0's total buffer (ptCommReduceSampleBufferInto) is
-  inside the timed region.  Per-GPU work per step is fixed: "weak".
-* bands (default for C4, "pixel-tiled across 8xMI355X"): the frame is split
-  into 16-row bands, band b on rank b % N (strong scaling: each rank traces
-  1/N of the frame); the frame-end RCCL point-to-point gather of every rank's
-  bands to rank 0 (ptCommGatherSampleBuffer) is inside the timed region.
+N GPUs, one process per GPU.  `bench.py --gpus N` without a launcher starts
+`torch.distributed.run --nproc-per-node N` over itself (before any GPU call);
+under a launcher WORLD_SIZE must equal --gpus.  The frame is split one of two
+ways (--shard), total work fixed either way ("strong" scaling):
+
+* samples (default, every config that fits one GPU): north_star's
+  "pixels/samples shard embarrassingly ... RCCL reduce of the per-pixel
+  radiance and sample-count buffers at frame end".  Every rank renders the
+  whole frame with its own RNG stream (FrameIndex offset rank << 24) to
+  1/N of the spp target; the frame-end ncclReduce of the XYZ sums and sample
+  counts into rank 0's total buffer (ptCommReduceSampleBufferInto) is inside
+  the step.
+* bands (default for C4, "pixel-tiled across 8xMI355X"): 16-row bands, band b
+  on rank b % N, each rank to the full spp target on its own pixels; the
+  frame-end RCCL point-to-point gather of the bands to rank 0
+  (ptCommGatherSampleBuffer) is inside the step.
 
 Prints ONE JSON line on rank 0.
 """
@@ -26,7 +34,10 @@ from __future__ import annotations
 import argparse
 import importlib.util
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -44,6 +55,8 @@ HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 ALG_BYTES = {"extend": 44, "shade": 176, "round": 220}   # round: fused extend + shade (small partitions)
 L2_PEAK_GBPS = 34500.0   # aggregate L2 bandwidth (MI355X_MICROARCH.md § L2)
 PATH_BYTES_PER_RAY = 220  # SURVEY.md §8(d) whole-path definition
+STEADY_ROUNDS = 64        # secondary key: steady-state rounds timed after the frames
+SETTLE_ROUNDS = 32        # ... after this many rounds past a restart
 
 
 def load_package():
@@ -55,29 +68,13 @@ def load_package():
     return mod
 
 
-SETTLE_ROUNDS = 32   # untimed rounds after Reset + Run(2), before the warm-up steps
-
-
-def measured_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC profile
-    (profiles/traffic.json <- profiles/pmc_summary.py over separate
-    FETCH_SIZE / WRITE_SIZE passes of this bench, gfx950-corrected), or None."""
-    p = ROOT / "profiles" / "traffic.json"
-    if not p.exists():
-        return None, None
-    d = json.loads(p.read_text())
-    k = d.get("kernels", {}).get(kernel, {})
-    return k.get("hbm_bytes"), d.get("profile")
-
-
-def measured_issue(kernel):
-    """VALU issue utilisation of `kernel` from the committed PMC profile
-    (profiles/traffic.json "issue"): the bound that actually limits the
-    traversal and shading kernels, which are far below the HBM roofline."""
+def profile_for(config):
+    """The committed PMC summary of this config's bench (profiles/traffic.json,
+    keyed by config; tools/update_traffic.py), or None."""
     p = ROOT / "profiles" / "traffic.json"
     if not p.exists():
         return None
-    return json.loads(p.read_text()).get("issue", {}).get(kernel)
+    return json.loads(p.read_text()).get("configs", {}).get(str(config))
 
 
 def cpu_model():
@@ -90,7 +87,7 @@ def cpu_model():
     return None
 
 
-def cpu_baseline(pt, scene, width, height, max_seconds=12.0, max_rounds=200):
+def cpu_baseline(pt, scene, width, height, config, max_seconds=12.0, max_rounds=200):
     """Time the CPU oracle (scalar C++ restatement, std::thread over host
     cores) on the same scene and frame.  Bounded: Reset + Run(2) warm-up, then
     single rounds until max_seconds of timed work or max_rounds.
@@ -122,42 +119,97 @@ def cpu_baseline(pt, scene, width, height, max_seconds=12.0, max_rounds=200):
     dt = time.perf_counter() - t0
     r1, s1 = o.counters()
     o.close()
+    share = "the job's CPU share (OMP_NUM_THREADS)" if omp > 0 and omp < allowed else "every affinity CPU"
     return {
         "value": round((r1 - r0) / dt / 1e6, 4),
         "unit": "Mrays/s",
         "cores": threads,
         "threads": threads,
+        "threads_used": f"{threads} threads = {share}; {allowed} affinity CPUs, {host_cpus} host CPUs",
         "host_cpus": host_cpus,
         "affinity_cpus": allowed,
         "omp_num_threads": omp or None,
         "cpu_model": cpu_model(),
         "kind": "port",
-        "sample": f"C3 {width}x{height}, {rounds} rounds after Reset+Run(2) warm-up "
-                  f"({(r1 - r0)} rays, {(s1 - s0)} samples, {dt:.1f} s)",
+        "sample": f"C{config} {width}x{height}, {rounds} rounds after Reset+Run(2) warm-up "
+                  f"({(r1 - r0)} rays, {(s1 - s0)} samples, {dt:.1f} s; the rate is stationary after the first "
+                  f"rounds, SURVEY.md §8(d))",
         "msamples_per_s": round((s1 - s0) / dt / 1e6, 4),
     }
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(n):
+    """`bench.py --gpus N` without a launcher: run torch.distributed.run over
+    this script as a child (no exec: nothing here has touched the GPU yet) and
+    exit with its status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(Path(__file__).resolve())] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def launch_check(args, world, rank):
+    """--launch-check: the N-rank plumbing without a GPU (CPU test of the
+    launcher): process group, world size, the max-over-ranks reduction and a
+    frame-end-sized gloo reduce; rank 0 prints the line's rank fields."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    acc = torch.ones(4 * 64 * 64, dtype=torch.float32)
+    dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
+    ok = (rank != 0) or bool(torch.all(acc == float(world)).item())
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "world_size": dist.get_world_size(),
+                          "max_over_ranks": float(t.item()), "reduce_ok": ok,
+                          "config": {"exchange": "gloo", "comm_ranks": dist.get_world_size()}}), flush=True)
+    dist.destroy_process_group()
+    return 0 if ok else 1
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=128)
-    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--steps", type=int, default=3, help="timed frames")
+    ap.add_argument("--warmup", type=int, default=1, help="untimed frames")
     ap.add_argument("--config", type=int, default=3)
-    ap.add_argument("--profile-period", type=int, default=4,
-                    help="time the kernels of every N-th step (HIP events) inside the timed loop")
+    ap.add_argument("--spp", type=int, default=0, help="frame spp target (default: the config's)")
+    ap.add_argument("--profile-period", type=int, default=8,
+                    help="time the kernels of every N-th round (HIP events) inside the timed frames")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-steady", action="store_true", help="skip the steady-state secondary measurement")
     ap.add_argument("--one-gpu-flow-check", action="store_true",
                     help="every rank on device 0 (multi-rank flow check on a one-GPU box; timings not meaningful)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="N-rank launch plumbing only (gloo, no GPU): CPU test of the launcher")
     ap.add_argument("--shard", choices=("auto", "samples", "bands"), default="auto",
                     help="multi-GPU split: samples (whole frame per rank, own RNG stream) or 16-row pixel bands; "
                          "auto = bands for C4 (pixel-tiled by its config), samples otherwise")
     args = ap.parse_args()
-    shard = args.shard if args.shard != "auto" else ("bands" if args.config == 4 else "samples")
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # N ranks: launch them first (before anything touches the GPU), or check
+    # the launcher's world size against --gpus.
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(self_launch(args.gpus))
+        world, rank, local_rank = 1, 0, 0
+    else:
+        world = int(os.environ["WORLD_SIZE"])
+        rank = int(os.environ.get("RANK", "0"))
+        local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        if world != args.gpus:
+            print(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr, flush=True)
+            sys.exit(2)
+    if args.launch_check:
+        sys.exit(launch_check(args, world, rank))
+
+    shard = args.shard if args.shard != "auto" else ("bands" if args.config == 4 else "samples")
     dist = None
     if world > 1:
         import torch
@@ -168,6 +220,7 @@ def main():
     scene = pt.Scene.config(args.config)
     info = scene.info
     width, height = info.width, info.height
+    spp = args.spp or info.spp
 
     # One GPU per rank: LOCAL_RANK indexes the visible devices; a launcher
     # that leaves each rank a single visible device gets device 0.
@@ -184,6 +237,10 @@ def main():
     # are hashed from (x, y, FrameIndex), scene.glsl.inc / basic.cpp:285-332).
     if shard == "samples":
         r.FrameIndex = rank << 24
+    slots_owned = int(np.sum(pt.owned_pixels(width, height, part_rank, part_n)))
+    # This rank's frame target (Σ alpha): samples -> 1/N of spp x frame,
+    # bands -> spp x its own pixels.
+    target = math.ceil(spp * width * height / world) if shard == "samples" else spp * slots_owned
     total = pt.SampleBuffer(dev, width, height) if (world > 1 and shard == "samples" and rank == 0) else None
     comm = None
     exchange = None
@@ -208,7 +265,7 @@ def main():
             comm, exchange = None, "gloo-fallback"
 
     def frame_end_exchange():
-        """The frame-end exchange (inside the timed region)."""
+        """The frame-end exchange (inside the step)."""
         if world == 1:
             return
         if comm is not None:
@@ -226,33 +283,32 @@ def main():
         if rank == 0:
             (total if shard == "samples" else sb).write(acc.numpy())
 
-    # Reset + Run(2) as after a restart (application.cpp:109-110), then the
-    # path population settles (the first ~30 rounds after a restart run ~4 %
-    # slower than the rest of a 1024-spp render, tools/exp_trend.py), then the
-    # W warm-up steps.
-    r.reset()
-    r.run(2)
-    r.run(SETTLE_ROUNDS)
-    for _ in range(args.warmup):
-        r.run(1)
-    dev.synchronize()
-    rays0, samples0 = r.stats()
-
     def barrier():
         if dist is not None:
             dist.barrier()
 
+    frames = []   # (rounds, samples) per timed frame
+
+    def frame(record):
+        rounds, samples = r.render_frame(target)
+        frame_end_exchange()
+        if record:
+            frames.append((rounds, samples))
+
+    for _ in range(args.warmup):
+        frame(False)
+    dev.synchronize()
+
     # Kernel durations: HIP events around the extend / shade launches of every
-    # profile_period-th step of the timed loop (an event pair per launch costs
-    # issue time; sampling keeps the measured loop representative).
+    # profile_period-th round of the timed frames (an event pair per launch
+    # costs issue time; sampling keeps the measured loop representative).
     dev.set_profiling(True, period=args.profile_period)
     dev.reset_kernel_stats()
     barrier()
     dev.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        r.run(1)
-    frame_end_exchange()
+        frame(True)
     dev.synchronize()
     barrier()
     dt = time.perf_counter() - t0
@@ -261,25 +317,44 @@ def main():
     n_rd, ms_rd = dev.kernel_stats(5)    # fused rounds (a partition that fits the GPU at once)
     dev.set_profiling(False)
 
+    rounds_local = sum(f[0] for f in frames)
+    samples_local = sum(f[1] for f in frames)
+    rays_local = rounds_local * slots_owned
+    assert all(f[1] >= target for f in frames), "a frame ended short of its spp target"
+
+    # Secondary: the steady-state rate (rounds after the path population
+    # settled, no Reset in the window), outside the timed frames.
+    steady = None
+    if not args.no_steady:
+        r.reset()
+        r.run(2)
+        for _ in range(SETTLE_ROUNDS):
+            r.run(1)
+        dev.synchronize()
+        s0 = time.perf_counter()
+        for _ in range(STEADY_ROUNDS):
+            r.run(1)
+        dev.synchronize()
+        sdt = time.perf_counter() - s0
+        steady = {"rounds": STEADY_ROUNDS, "after_rounds": SETTLE_ROUNDS + 2,
+                  "ms_per_round": round(sdt / STEADY_ROUNDS * 1e3, 4),
+                  "mrays_per_s_per_gpu": round(slots_owned * STEADY_ROUNDS / sdt / 1e6, 3)}
+
     # Traversal counters of one extra extend over the current rays (outside
     # the timed region; the next Run overwrites the same hit records).
     trav = r.extend_stats()
-    slots_owned = int(np.sum(pt.owned_pixels(width, height, part_rank, part_n)))
-    # Rays traced and paths completed in the timed steps (ptGetStats; the
-    # sample count equals the accumulator's alpha increments).
-    rays1, samples1 = r.stats()
-    rays_local, samples_local = rays1 - rays0, samples1 - samples0
-    assert rays_local == slots_owned * args.steps
     if dist is not None:
         import torch
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        local = torch.tensor([rays_local, samples_local], dtype=torch.float64)
+        local = torch.tensor([rays_local, samples_local, rounds_local], dtype=torch.float64)
         dist.all_reduce(local, op=dist.ReduceOp.SUM)
-        rays, samples = float(local[0]), float(local[1])
+        rays, samples, rounds_all = float(local[0]), float(local[1]), float(local[2])
+        comm_ranks = world if comm is not None else None
     else:
-        rays, samples = float(rays_local), float(samples_local)
+        rays, samples, rounds_all = float(rays_local), float(samples_local), float(rounds_local)
+        comm_ranks = None
 
     def shutdown():
         for x in (r, sb, dscene) + ((total,) if total is not None else ()):
@@ -303,10 +378,15 @@ def main():
             kernels[name] = {"avg_ms": avg, "gbps": ALG_BYTES[name] * slots_owned / (avg * 1e-3) / 1e9}
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
     achieved = kernels[dom]["gbps"]
-    traffic, traffic_src = measured_traffic(dom)
+    prof = profile_for(args.config) or {}
+    kprof = prof.get("kernels", {}).get(dom, {})
+    # The committed PMC profile holds the N=1 whole-frame launches; a band
+    # partition's launches cover 1/N of the slots, so its per-launch bytes do
+    # not apply.
+    traffic = kprof.get("hbm_bytes") if part_n == 1 else None
     xname = "RCCL" if exchange == "rccl" else "gloo (host-memory fallback)"
-    metric = ("Mrays/s + Msamples/s, Viking Room 1920x1080 1024spp, 1/2/4/8 GPUs" if args.config == 3 else
-              f"Mrays/s + Msamples/s, C{args.config} {info.width}x{info.height} {info.spp}spp")
+    metric = ("Mrays/s + Msamples/s, Viking Room 1920x1080 1024spp, 1/2/4/8 GPUs" if args.config == 3 and spp == 1024
+              else f"Mrays/s + Msamples/s, C{args.config} {info.width}x{info.height} {spp}spp")
     out = {
         "metric": metric,
         "value": round(mrays, 3),
@@ -314,24 +394,27 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(dt / args.steps * 1e3, 4),
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak" if shard == "samples" else "strong",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "data": f"synthetic (procedural {info.mesh_face_count}-triangle room mesh + 1024^2 texture; "
                 "Viking Room asset absent)",
         "config": {
-            "workload": (f"C{args.config} scene, {width}x{height} px frame split in 16-row bands over {world} GPU(s) "
-                         f"({slots_owned} px on rank 0), one round (extend+shade of every pixel's path) per step"
+            "workload": (f"C{args.config} scene, one {width}x{height} {spp}-spp frame per step (Reset, Run(2), "
+                         f"Run(1) until the frame's sample count reaches {spp} x pixels), split in 16-row bands over "
+                         f"{world} GPU(s) ({slots_owned} px on rank 0) + the bands' gather to rank 0"
                          if shard == "bands" else
-                         f"C{args.config} scene, {width}x{height} px frame; each of {world} GPU(s) renders every pixel "
-                         f"with its own RNG stream (the spp target split over the GPUs), one round (extend+shade of "
-                         f"every pixel's path) per step per GPU"),
+                         f"C{args.config} scene, one {width}x{height} {spp}-spp frame per step (Reset, Run(2), "
+                         f"Run(1) until the frame's sample count reaches {spp} x pixels); each of {world} GPU(s) "
+                         f"renders every pixel with its own RNG stream to 1/{world} of the samples, then the "
+                         f"reduce of radiance + sample counts to rank 0"),
             "shard": shard,
             "exchange": exchange,
-            "spp_target": info.spp,
-            "settle_rounds": SETTLE_ROUNDS,
+            "comm_ranks": comm_ranks,
+            "spp_target": spp,
+            "frame_target_samples_rank0": target,
             "mesh_faces": info.mesh_face_count,
             "parallelism": (f"pixel-bands x{world}" + (f" + {xname} band gather to rank 0" if world > 1 else "")
                             if shard == "bands" else
@@ -339,6 +422,15 @@ def main():
                                                          if world > 1 else "")),
         },
         "msamples_per_s": round(samples / dt / 1e6, 3),
+        "frame": {
+            "frame_s": round(dt / args.steps, 4),
+            "rounds_per_frame_rank0": [f[0] for f in frames],
+            "rounds_all_ranks": int(rounds_all),
+            "samples_per_frame_rank0": [f[1] for f in frames],
+            "rays": int(rays),
+            "samples": int(samples),
+        },
+        "steady_state": steady,
         "roofline": {
             "bound": "hbm",
             "kernel": dom,
@@ -348,19 +440,20 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBPS, 5),
             "traffic": traffic,
             "traffic_unit": "bytes per launch (HBM, PMC)",
-            "traffic_source": traffic_src,
+            "traffic_source": prof.get("profile") if traffic is not None else None,
             "alg_bytes_per_launch": ALG_BYTES[dom] * slots_owned,
             "alg_bytes_per_slot": ALG_BYTES[dom],
             "launch_avg_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
-            "launches_timed": {"extend": n_ext, "shade": n_sh, "round": n_rd, "every_nth_step": args.profile_period},
+            "launches_timed": {"extend": n_ext, "shade": n_sh, "round": n_rd, "every_nth_round": args.profile_period},
             "path_gbps_220B_per_ray": round(PATH_BYTES_PER_RAY * rays / dt / 1e9, 2),
         },
-        # What bounds the dominant kernel instead of HBM (PMC, same profile):
-        # fraction of the chip's VALU issue slots used, and active lanes per
-        # VALU instruction (of 64; divergence).
-        "limiter": {"kind": "valu_issue", "kernel": dom, **(measured_issue(dom) or {}),
-                    "per_kernel": {k: measured_issue(k) for k in ("extend", "shade")},
-                    "source": traffic_src},
+        # What bounds the dominant kernel instead of HBM (PMC of this config's
+        # committed profile): fraction of the chip's VALU issue slots used and
+        # active lanes per VALU instruction (of 64; divergence).  null when no
+        # profile of this config is committed.
+        "limiter": ({"kind": "valu_issue", "kernel": dom, **(prof.get("issue", {}).get(dom) or {}),
+                     "per_kernel": {k: prof.get("issue", {}).get(k) for k in ("extend", "shade")},
+                     "source": prof.get("profile")} if prof and part_n == 1 else None),
     }
     # Node/face bytes the traversal pulls through L1/L2 per ray (BVH + faces
     # are cache-resident): internal node = both child boxes (64 B), face 48 B,
@@ -378,7 +471,7 @@ def main():
         "l2_peak_gbps": L2_PEAK_GBPS,
     }
     if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only
-        out["cpu_baseline"] = cpu_baseline(pt, scene, info.width, info.height)
+        out["cpu_baseline"] = cpu_baseline(pt, scene, info.width, info.height, args.config)
     print(json.dumps(out), flush=True)
     shutdown()
 

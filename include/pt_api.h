@@ -209,6 +209,14 @@ int                ptSetBasicRendererOpenPBR(pt_basic_renderer* renderer, int en
  * and paths completed (accumulator sample increments, basic_scatter.glsl:
  * 350-359).  Either pointer may be NULL.  Synchronises the device stream. */
 int                ptGetStats(pt_device* device, pt_basic_renderer* renderer, uint64_t* rays, uint64_t* samples);
+/* Benchmark-mode frame (no reference entry point: the
+ * application loop of application.cpp:100-115 with an spp target): Reset,
+ * Run(2), then Run(1) rounds until the paths completed since the Reset reach
+ * target_samples (e.g. spp * pixels owned) or max_rounds (>= 2) rounds ran.
+ * Blocks until done.  rounds_out / samples_out (either may be NULL): rounds
+ * run and paths completed. */
+int                ptRenderFrame(pt_device* device, pt_basic_renderer* renderer, uint64_t target_samples,
+                                 uint32_t max_rounds, uint32_t* rounds_out, uint64_t* samples_out);
 /* out = width*height states in image order; pixels outside the renderer's
  * partition are left untouched. */
 int                ptReadBasicRendererState(pt_device* device, pt_basic_renderer* renderer, pt_pixel_state* out);
@@ -258,9 +266,10 @@ int ptExtendStepCounts(pt_device* device, pt_basic_renderer* renderer, uint32_t*
 
 /* Per-kernel device time, measured with HIP events on the renderer stream. */
 int ptSetProfiling(pt_device* device, int enable);
-/* Time only every period-th ptRunBasicRenderer call (default 1): each event
- * pair around a kernel costs issue time, so a timed loop can sample its
- * kernels' durations instead of bracketing every launch. */
+/* Time only the kernels of every period-th round (default 1; rounds counted
+ * across ptRunBasicRenderer calls): each event pair around a kernel costs
+ * issue time, so a timed loop can sample its kernels' durations instead of
+ * bracketing every launch. */
 int ptSetProfilingPeriod(pt_device* device, uint32_t period);
 int ptGetKernelStats(pt_device* device, int kernel, uint64_t* launches, double* total_ms);
 int ptResetKernelStats(pt_device* device);

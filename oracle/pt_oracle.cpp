@@ -123,15 +123,25 @@ pt3 UnpackUnitVector(uint32_t PackedV)                                          
     return normalize(v3(P.x, P.y, Z));
 }
 
-// The division (Min - Ray.Origin) / Ray.Velocity is evaluated as
-// RN((Min - Ray.Origin) * RN(1 / Ray.Velocity)): GLSL allows `/` 2.5 ULP and
-// GPU compilers emit this reciprocal form for it (numerics convention,
-// DESIGN.md §2); the HIP slab test evaluates the same expression.
+// Slab-test division convention (process-wide; oracle_set_slab_division).
+// 1 (default, the HIP kernels' convention and SURVEY.md §7/§8(c)'s):
+// correctly rounded IEEE (Min - Ray.Origin) / Ray.Velocity.  0: the
+// reciprocal form RN((Min - Ray.Origin) * RN(1 / Ray.Velocity)) GPU compilers
+// emit for GLSL's 2.5-ULP `/`; kept to measure what that form changes
+// (tools/slab_convention.py, tests/test_slab_convention.py).
+std::atomic<int> SlabDivisionIEEE{1};
+
 float IntersectBoundingBox(const ray& Ray, float Reach, pt3 Min, pt3 Max)                            // :153-185
 {
-    pt3 InverseVelocity = v3(1.0f / Ray.Velocity.x, 1.0f / Ray.Velocity.y, 1.0f / Ray.Velocity.z);
-    pt3 MinT = (Min - Ray.Origin) * InverseVelocity;
-    pt3 MaxT = (Max - Ray.Origin) * InverseVelocity;
+    pt3 MinT, MaxT;
+    if (SlabDivisionIEEE.load(std::memory_order_relaxed)) {
+        MinT = (Min - Ray.Origin) / Ray.Velocity;                                                    // :157-158
+        MaxT = (Max - Ray.Origin) / Ray.Velocity;
+    } else {
+        pt3 InverseVelocity = v3(1.0f / Ray.Velocity.x, 1.0f / Ray.Velocity.y, 1.0f / Ray.Velocity.z);
+        MinT = (Min - Ray.Origin) * InverseVelocity;
+        MaxT = (Max - Ray.Origin) * InverseVelocity;
+    }
     pt3 EarlierT = vmin(MinT, MaxT);
     pt3 LaterT = vmax(MinT, MaxT);
     float EntryT = pt_max(pt_max(EarlierT.x, EarlierT.y), EarlierT.z);
@@ -1447,6 +1457,17 @@ oracle_renderer* oracle_create(const pt_scene_packs* packs, uint32_t width, uint
 void oracle_destroy(oracle_renderer* r) { delete r; }
 pt_basic_renderer_params* oracle_params(oracle_renderer* r) { return &r->Params; }
 void oracle_set_openpbr(oracle_renderer* r, int enable) { r->OpenPBR = enable != 0; }
+void oracle_set_slab_division(int ieee) { SlabDivisionIEEE.store(ieee != 0); }
+int oracle_slab_division(void) { return SlabDivisionIEEE.load(); }
+float oracle_intersect_bounding_box(const float origin[3], const float velocity[3], float reach, const float mn[3],
+                                    const float mx[3])
+{
+    ray R;
+    R.Origin = v3(origin[0], origin[1], origin[2]);
+    R.Velocity = v3(velocity[0], velocity[1], velocity[2]);
+    R.Duration = reach;
+    return IntersectBoundingBox(R, reach, v3(mn[0], mn[1], mn[2]), v3(mx[0], mx[1], mx[2]));
+}
 
 // ResetBasicRenderer (basic.cpp:285-304): one scatter dispatch, Restart=1,
 // seeded with the current FrameIndex.

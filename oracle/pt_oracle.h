@@ -30,6 +30,15 @@ void oracle_destroy(oracle_renderer* r);
 pt_basic_renderer_params* oracle_params(oracle_renderer* r);
 /* OpenPBR shading on/off (ptSetBasicRendererOpenPBR); off by default. */
 void oracle_set_openpbr(oracle_renderer* r, int enable);
+/* Slab-test division convention for every later Trace() in this process:
+ * 1 = correctly rounded IEEE (Min-O) / V (default: the HIP kernels' and
+ * SURVEY.md §7/§8(c)'s convention), 0 = reciprocal multiply
+ * RN((Min-O) * RN(1/V)) (measurement only). */
+void oracle_set_slab_division(int ieee);
+int oracle_slab_division(void);
+/* IntersectBoundingBox (common.glsl.inc:153-185) in the current convention: entry t or 1e30. */
+float oracle_intersect_bounding_box(const float origin[3], const float velocity[3], float reach, const float mn[3],
+                                    const float mx[3]);
 void oracle_reset(oracle_renderer* r);
 void oracle_run(oracle_renderer* r, uint32_t rounds);
 void oracle_read_accum(oracle_renderer* r, float* rgba);

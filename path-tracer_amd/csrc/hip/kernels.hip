@@ -26,6 +26,9 @@
 #include "kernels.hpp"
 
 #include <type_traits>
+#include <map>
+#include <mutex>
+#include <tuple>
 
 namespace ptd {
 
@@ -1522,13 +1525,24 @@ static const void* RoundKernelFor(uint32_t mats, bool stack16)
 uint32_t pt_round_capacity(uint32_t scene_mats, bool stack16, uint32_t cu_count)
 {
     if (pt_extend_variant() != 0) return 0;   // round_kernel has the default variant's 20-entry stack
-    static int per_cu[4][2] = {{-1, -1}, {-1, -1}, {-1, -1}, {-1, -1}};   // by shade mask, stack entry width
+    // Blocks per CU of the round kernel instantiation, cached per (device,
+    // shade mask, stack entry width); renderers may be created from several
+    // host threads and on several devices.
+    static std::mutex mu;
+    static std::map<std::tuple<int, uint32_t, bool>, int> per_cu;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
     uint32_t m = pt_shade_mats(scene_mats);
-    int& c = per_cu[m == PT_MATS_DIFFUSE ? 0 : m == (PT_MATS_DIFFUSE | PT_MATS_METAL) ? 1 : m == PT_MATS_ALL ? 2 : 3]
-                   [stack16 ? 1 : 0];
-    if (c < 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(&c, RoundKernelFor(scene_mats, stack16), 256, 0) != hipSuccess)
-        c = 0;
-    return (uint32_t)c * cu_count;
+    std::lock_guard<std::mutex> lock(mu);
+    auto key = std::make_tuple(dev, m, stack16);
+    auto it = per_cu.find(key);
+    if (it == per_cu.end()) {
+        int c = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&c, RoundKernelFor(scene_mats, stack16), 256, 0) != hipSuccess)
+            c = 0;
+        it = per_cu.emplace(key, c).first;
+    }
+    return (uint32_t)it->second * cu_count;
 }
 
 hipError_t pt_launch_round(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,

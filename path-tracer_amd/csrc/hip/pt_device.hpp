@@ -37,6 +37,7 @@ struct dscene {
     const float4* atlas;
     uint32_t atlas_w, atlas_h, atlas_layers;
     uint32_t atlas_tiled;          // atlas stored in 4x2-texel blocks (AtlasIndex), not row-major
+    uint32_t fast_div;             // every BVH box coordinate is 0 or in [2^-50, 2^40] (IntersectBoundingBox)
     uint32_t blas_words;           // BLAS stack entry format: 0 node index, 1 packed words (PackBlasEntry),
                                    // 2 16-bit packed words (PackBlasEntry16, blas_firstbits)
     uint32_t blas_firstbits;       // format 2: bits of a leaf's first face index (count above them)
@@ -106,9 +107,8 @@ PT_DEV pt3 UnpackUnitVector(uint32_t P)
 // correction (Markstein) -> RN(a/b).  Outside the guarded range (b or a/b
 // beyond 2^+-100, b = 0, a = 0, NaN) it falls back to IEEE division, so the
 // result is always bit-identical to a / b; ptCheckFastDivision verifies this
-// over >10^9 operand pairs on the device.  (The slab test used it until the
-// reciprocal convention below; it remains a checked helper for exact
-// quotients at reciprocal cost.)
+// over >10^9 operand pairs on the device.  (The slab test uses the same
+// correction without a per-quotient guard: FastQuot below.)
 PT_DEV float RecipForDiv(float b)
 {
     float m = pt_abs(b);
@@ -159,29 +159,73 @@ PT_DEV bool FastRcpRange(float d)
 }
 
 
-// Slab test (common.glsl.inc:153-185).  Its division (Min - O) / V is
-// evaluated as RN((Min - O) * Y) with Y = RN(1/V), computed once per ray and
-// traversal level (numerics convention, DESIGN.md §2: GLSL gives `/` 2.5 ULP
-// and GPU compilers emit this reciprocal form for it; the oracle evaluates
-// the same expression).  A zero velocity component makes Y infinite and a
-// plane through the origin gives 0 * inf = NaN, which minnum / maxnum drop
-// as fminf / fmaxf do.
-PT_DEV float IntersectBoundingBox(pt3 O, pt3 Y, float Reach, float4 MinAndX, float4 MaxAndX)
+// Exact fast slab division.  With y = RN(1/b), q = RN(a*y), r = fma(-q,b,a),
+// q' = fma(r,y,q) equals IEEE a/b whenever r is exact and q, r*y, q' stay
+// normal (Markstein).  That holds for every plane of every box if
+//   * every box coordinate and ray-origin component is 0 or has magnitude in
+//     [2^-50, 2^40]  ->  every nonzero a = Min - O has |a| >= 2^-73, |a| <= 2^41
+//   * every ray-velocity component has magnitude in [2^-59, 2^27]
+// so |a/b| lies in [2^-100, 2^100] and r is exact (|a| >= 2^-103).  a = 0
+// gives q' = +-0, whose sign may differ from IEEE's; the slab test only
+// compares its quotients, where -0 == +0.  The box-coordinate condition is
+// checked once per scene on the host (dscene::fast_div), the ray condition
+// once per ray and traversal level (FastDivRay); rays outside it take IEEE
+// division.  No NaN reaches the fast path, so plain hardware min/max give the
+// same comparisons as fminf/fmaxf.
+PT_DEV bool FastDivRay(pt3 O, pt3 V)
 {
-    pt3 A = xyz(MinAndX) - O, B = xyz(MaxAndX) - O;
-    float ax = A.x * Y.x, ay = A.y * Y.y, az = A.z * Y.z;
-    float bx = B.x * Y.x, by = B.y * Y.y, bz = B.z * Y.z;
+    bool ok = true;
+#define PT_CHECK_O(c) { float m = pt_abs(c); ok &= (m == 0.0f) | ((m >= 0x1p-50f) & (m <= 0x1p40f)); }
+#define PT_CHECK_V(c) { float m = pt_abs(c); ok &= (m >= 0x1p-59f) & (m <= 0x1p27f); }
+    PT_CHECK_O(O.x) PT_CHECK_O(O.y) PT_CHECK_O(O.z)
+    PT_CHECK_V(V.x) PT_CHECK_V(V.y) PT_CHECK_V(V.z)
+#undef PT_CHECK_O
+#undef PT_CHECK_V
+    return ok;
+}
+
+PT_DEV float FastQuot(float a, float b, float y)
+{
+    float q = a * y;
+    float r = __builtin_fmaf(-q, b, a);
+    return __builtin_fmaf(r, y, q);
+}
+
+// Slab test (common.glsl.inc:153-185) with IEEE division (Min - O) / V, the
+// numerics convention of SURVEY.md §7/§8(c).  `exact`: the
+// lane's ray satisfies FastDivRay and the scene's boxes the coordinate
+// condition, so FastQuot gives the IEEE quotients; otherwise true division.
+// With true division a zero velocity component and a plane through the
+// origin give 0 / 0 = NaN, which minnum / maxnum drop as fminf / fmaxf do.
+PT_DEV float SlabEntry(float ax, float ay, float az, float bx, float by, float bz, float Reach)
+{
     float EntryT = HwMax3(HwMin(ax, bx), HwMin(ay, by), HwMin(az, bz));
     float ExitT = HwMin3(HwMax(ax, bx), HwMax(ay, by), HwMax(az, bz));
     bool miss = (ExitT < EntryT) | (ExitT <= 0.0f) | (EntryT >= Reach);
     return miss ? PT_INFINITY : EntryT;
 }
 
-// Both child boxes of an internal node.
-PT_DEV void IntersectBoxPair(pt3 O, pt3 Y, float Reach, float4 a0, float4 a1, float4 b0, float4 b1, float& TA, float& TB)
+PT_DEV float IntersectBoundingBox(pt3 O, pt3 V, pt3 Y, float Reach, float4 MinAndX, float4 MaxAndX, bool exact)
 {
-    TA = IntersectBoundingBox(O, Y, Reach, a0, a1);
-    TB = IntersectBoundingBox(O, Y, Reach, b0, b1);
+    pt3 A = xyz(MinAndX) - O, B = xyz(MaxAndX) - O;
+    if (exact)
+        return SlabEntry(FastQuot(A.x, V.x, Y.x), FastQuot(A.y, V.y, Y.y), FastQuot(A.z, V.z, Y.z),
+                         FastQuot(B.x, V.x, Y.x), FastQuot(B.y, V.y, Y.y), FastQuot(B.z, V.z, Y.z), Reach);
+    return SlabEntry(A.x / V.x, A.y / V.y, A.z / V.z, B.x / V.x, B.y / V.y, B.z / V.z, Reach);
+}
+
+// Both child boxes of an internal node under one `exact` branch (one
+// divergent branch per node instead of one per box).
+PT_DEV void IntersectBoxPair(pt3 O, pt3 V, pt3 Y, float Reach, float4 a0, float4 a1, float4 b0, float4 b1, bool exact,
+                             float& TA, float& TB)
+{
+    if (exact) {
+        TA = IntersectBoundingBox(O, V, Y, Reach, a0, a1, true);
+        TB = IntersectBoundingBox(O, V, Y, Reach, b0, b1, true);
+    } else {
+        TA = IntersectBoundingBox(O, V, Y, Reach, a0, a1, false);
+        TB = IntersectBoundingBox(O, V, Y, Reach, b0, b1, false);
+    }
 }
 
 struct rng {

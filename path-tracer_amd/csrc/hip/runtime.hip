@@ -448,6 +448,24 @@ void ptDestroyScene(pt_device* d, pt_scene* s)
 }
 
 // UpdateVulkanScene (scene.cpp:1692-2006): synchronous upload of the packs.
+// Box-coordinate condition of the extend kernel's exact fast slab division
+// (pt_device.hpp, IntersectBoundingBox): every TLAS / BLAS bound is 0 or has
+// magnitude in [2^-50, 2^40].  Scenes outside it trace with IEEE division.
+static bool FastDivBoxes(const pt_scene_packs* p)
+{
+    auto ok = [](float c) {
+        float m = std::fabs(c);
+        return m == 0.0f || (m >= 0x1p-50f && m <= 0x1p40f);
+    };
+    for (uint32_t i = 0; i < p->shape_node_count; i++)
+        for (int k = 0; k < 3; k++)
+            if (!ok(p->shape_nodes[i].Minimum[k]) || !ok(p->shape_nodes[i].Maximum[k])) return false;
+    for (uint32_t i = 0; i < p->mesh_node_count; i++)
+        for (int k = 0; k < 3; k++)
+            if (!ok(p->mesh_nodes[i].Minimum[k]) || !ok(p->mesh_nodes[i].Maximum[k])) return false;
+    return true;
+}
+
 // Whether every BLAS node's index words fit one packed stack entry
 // (PackBlasEntry): leaves with <= 31 faces starting below 2^26, child-pair
 // indices below 2^31.  PT_BLAS_WORDS=0 forces the index form (A/B testing).
@@ -585,6 +603,7 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     D.atlas_h = p->atlas_height;
     D.atlas_layers = p->atlas ? p->atlas_layer_count : 0;
     D.atlas_tiled = s->atlas_tiled ? 1u : 0u;
+    D.fast_div = FastDivBoxes(p) ? 1u : 0u;
     s->mats = SceneMaterialMask(p);
     uint32_t types = s->mats & (PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_TRANSLUCENT | PT_MATS_OPENPBR);
     D.mat_classes = (types & (types - 1)) != 0 ? 1u : 0u;   // more than one material type
@@ -889,7 +908,6 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
     r->params.FrameIndex += 1;
     ptd::dparams P = Params(r, r->params.FrameIndex);
     ptd::dframe F = Frame(r);
-    bool sampled = d->profiling && (d->run_tick++ % d->profile_period) == 0;
     const uint32_t G = r->groups, tiles = r->slots.n / 256;
     // Group g: tiles [tiles*g/G, tiles*(g+1)/G) on its own stream, forked from
     // and joined back into the device stream (ordering with Reset, scene
@@ -907,35 +925,48 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
         PT_HIP(hipEventRecord(r->fork, d->stream));
         for (uint32_t g = 0; g < G; g++) PT_HIP(hipStreamWaitEvent(st[g], r->fork, 0));
     }
-    for (uint32_t i = 0; i < rounds; i++) {
-        // Tiles keep their relative cost for many rounds: re-sort every
-        // TileOrderPeriod() rounds (the sort is one small launch per group).
-        bool sort = r->slots.order && (r->order_tick++ % TileOrderPeriod()) == 0;
-        for (uint32_t g = 0; g < G; g++) {
-            event_pair ep{};
-            if (RoundFused(r, gs[g])) {
-                if (int e = BeginTimed(d, PT_KERNEL_ROUND, ep, sampled, st[g])) return e;
-                PT_HIP(pt_launch_round(r->scene->d, gs[g], F, P, ShadeMats(r), st[g]));
+    // The group streams join the device stream on every exit, error paths
+    // included, so that later reads and Destroy (which synchronise the device
+    // stream only) never overlap group work.
+    auto join = [&]() -> int {
+        if (G > 1)
+            for (uint32_t g = 0; g < G; g++) {
+                PT_HIP(hipEventRecord(r->gevent[g], st[g]));
+                PT_HIP(hipStreamWaitEvent(d->stream, r->gevent[g], 0));
+            }
+        return 0;
+    };
+    auto rounds_loop = [&]() -> int {
+        for (uint32_t i = 0; i < rounds; i++) {
+            // Kernel timing samples every profile_period-th round.
+            bool sampled = d->profiling && (d->run_tick++ % d->profile_period) == 0;
+            // Tiles keep their relative cost for many rounds: re-sort every
+            // TileOrderPeriod() rounds (the sort is one small launch per group).
+            bool sort = r->slots.order && (r->order_tick++ % TileOrderPeriod()) == 0;
+            for (uint32_t g = 0; g < G; g++) {
+                event_pair ep{};
+                if (RoundFused(r, gs[g])) {
+                    if (int e = BeginTimed(d, PT_KERNEL_ROUND, ep, sampled, st[g])) return e;
+                    PT_HIP(pt_launch_round(r->scene->d, gs[g], F, P, ShadeMats(r), st[g]));
+                    if (int e = EndTimed(d, ep)) return e;
+                    if (sort) PT_HIP(pt_launch_tile_order(gs[g], st[g]));
+                    continue;
+                }
+                if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled, st[g])) return e;
+                PT_HIP(pt_launch_extend(r->scene->d, gs[g], F, r->slots.spill, st[g]));
+                if (int e = EndTimed(d, ep)) return e;
+                if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled, st[g])) return e;
+                PT_HIP(pt_launch_shade(r->scene->d, gs[g], F, P, ShadeMats(r), st[g]));
                 if (int e = EndTimed(d, ep)) return e;
                 if (sort) PT_HIP(pt_launch_tile_order(gs[g], st[g]));
-                continue;
             }
-            if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled, st[g])) return e;
-            PT_HIP(pt_launch_extend(r->scene->d, gs[g], F, r->slots.spill, st[g]));
-            if (int e = EndTimed(d, ep)) return e;
-            if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled, st[g])) return e;
-            PT_HIP(pt_launch_shade(r->scene->d, gs[g], F, P, ShadeMats(r), st[g]));
-            if (int e = EndTimed(d, ep)) return e;
-            if (sort) PT_HIP(pt_launch_tile_order(gs[g], st[g]));
+            r->rays += r->pixels;
         }
-        r->rays += r->pixels;
-    }
-    if (G > 1)
-        for (uint32_t g = 0; g < G; g++) {
-            PT_HIP(hipEventRecord(r->gevent[g], st[g]));
-            PT_HIP(hipStreamWaitEvent(d->stream, r->gevent[g], 0));
-        }
-    return 0;
+        return 0;
+    };
+    int e = rounds_loop();
+    int j = join();
+    return e ? e : j;
 }
 
 uint32_t ptBasicRendererRunGroups(pt_basic_renderer* r) { return r ? r->groups : 0; }
@@ -971,6 +1002,48 @@ int ptGetStats(pt_device* d, pt_basic_renderer* r, uint64_t* rays, uint64_t* sam
         for (uint32_t v : w) sum += v;
         *samples = sum;
     }
+    return 0;
+}
+
+// Benchmark-mode frame: Reset, Run(2) as after a restart
+// (application.cpp:109-110), then Run(1) rounds -- one new seed each, as the
+// application's frame loop issues them (application.cpp:100-115,
+// basic.cpp:306-332) -- until the paths completed since the Reset reach
+// target_samples (the accumulator's alpha sum) or max_rounds rounds ran.
+// The completed count is read back between batches of rounds: a batch is
+// never longer than the rounds that could not reach the target even if every
+// slot completed a path each round, or than 90 % of the rounds the last
+// batch's completion rate predicts -- so the frame ends at (or, if the rate
+// jumps by > 10 % within a batch, a few rounds after) the reference's round.
+int ptRenderFrame(pt_device* d, pt_basic_renderer* r, uint64_t target_samples, uint32_t max_rounds,
+                  uint32_t* rounds_out, uint64_t* samples_out)
+{
+    if (!d || !r) { SetError("null argument"); return -1; }
+    if (max_rounds < 2) { SetError("ptRenderFrame: max_rounds must be >= 2"); return -1; }
+    if (int e = ptResetBasicRenderer(d, r)) return e;
+    if (int e = ptRunBasicRenderer(d, r, 2)) return e;
+    uint32_t rounds = 2;
+    uint64_t samples = 0, prev = 0;
+    uint32_t last_batch = 0;
+    const uint64_t px = std::max<uint64_t>(r->pixels, 1);
+    for (;;) {
+        if (int e = ptGetStats(d, r, nullptr, &samples)) return e;
+        if (samples >= target_samples || rounds >= max_rounds) break;
+        uint64_t remaining = target_samples - samples;
+        uint64_t k = (remaining + px - 1) / px;                      // cannot overshoot
+        if (last_batch > 0 && samples > prev) {
+            double rate = (double)(samples - prev) / last_batch;     // completions per round
+            k = std::max<uint64_t>(k, (uint64_t)(0.9 * (double)remaining / rate));
+        }
+        k = std::max<uint64_t>(1, std::min<uint64_t>(k, max_rounds - rounds));
+        for (uint64_t i = 0; i < k; i++)
+            if (int e = ptRunBasicRenderer(d, r, 1)) return e;
+        rounds += (uint32_t)k;
+        prev = samples;
+        last_batch = (uint32_t)k;
+    }
+    if (rounds_out) *rounds_out = rounds;
+    if (samples_out) *samples_out = samples;
     return 0;
 }
 
@@ -1323,6 +1396,21 @@ void ptCommDestroy(pt_comm* c)
 int ptCommReduceSampleBuffer(pt_device* d, pt_comm* c, pt_sample_buffer* b, int root)
 {
     if (!d || !c || !b) { SetError("null argument"); return -1; }
+    if (root < 0 || root >= c->nranks) { SetError("bad root %d", root); return -1; }
+    // The rows zeroed below are those outside the buffer's partition, so the
+    // partition must be this communicator's rank of nranks.  A whole-frame
+    // buffer on a multi-rank communicator is a sample shard: reducing it in
+    // place would add the root's previous totals again on a repeated call.
+    if (b->nranks == 1 && c->nranks > 1) {
+        SetError("ptCommReduceSampleBuffer: whole-frame buffer on a %d-rank communicator (sample shards: use "
+                 "ptCommReduceSampleBufferInto)", c->nranks);
+        return -1;
+    }
+    if (b->nranks > 1 && ((int)b->nranks != c->nranks || (int)b->rank != c->rank)) {
+        SetError("sample buffer partition %u/%u does not match communicator rank %d of %d", b->rank, b->nranks,
+                 c->rank, c->nranks);
+        return -1;
+    }
     PT_HIP(hipSetDevice(d->id));
     size_t count = (size_t)b->width * b->height * 4;
     // Only the bands this rank renders may enter the sum: at the root the

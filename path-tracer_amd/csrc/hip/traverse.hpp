@@ -60,6 +60,7 @@ struct lane_state {
                          // BLAS {FaceBeginOrNodeIndex, FaceEndIndex}
     uint32_t dT, dB;     // TLAS / BLAS stack depths (<= 32 each)
     uint32_t blas;       // shape index of the mesh being traversed, NONE at TLAS level
+    bool exact;          // fast exact slab division applies to the current-level ray
     uint32_t HA, HB;     // hit's mesh face vertex indices, 3 x 21 bits (PackVertexIndices);
                          // an analytic shape's hit: HA = C.x (CompactHit)
 };
@@ -68,6 +69,7 @@ PT_DEV void SetLevelRay(const dscene& S, lane_state& L, pt3 O, pt3 V)
 {
     L.O = O;
     L.V = V;
+    L.exact = S.fast_div && FastDivRay(O, V);
 #if PT_FAST_RCP
     L.Y = v3(FastRcp(V.x), FastRcp(V.y), FastRcp(V.z));
     if (!(FastRcpRange(V.x) & FastRcpRange(V.y) & FastRcpRange(V.z))) L.Y = v3(1.0f / V.x, 1.0f / V.y, 1.0f / V.z);
@@ -97,6 +99,7 @@ PT_DEV void LaneBegin(const dscene& S, lane_state& L, pt3 O, pt3 V, float Durati
         // reciprocal; the world-space one would never be read.
         L.O = O;
         L.V = V;
+        L.exact = false;
         asm("" : "=v"(L.Y.x), "=v"(L.Y.y), "=v"(L.Y.z));
     }
 }
@@ -398,7 +401,7 @@ PT_DEV bool TlasStep(const dscene& S, lane_state& L, tstack<SPILL, CAP, SE>& st,
             const float4* Bp = S.shape_nodes + 2 * (size_t)IB;
             float4 a0 = Ap[0], a1 = Ap[1], b0 = Bp[0], b1 = Bp[1];
             float TA, TB;
-            IntersectBoxPair(L.O, L.Y, L.Time, a0, a1, b0, b1, TA, TB);
+            IntersectBoxPair(L.O, L.V, L.Y, L.Time, a0, a1, b0, b1, L.exact, TA, TB);
             // Same decision as the BLAS step (scene.glsl.inc:494-516).
             bool goB = TA > TB;
             bool any = goB | (TA < PT_INFINITY);
@@ -466,7 +469,7 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP, SE>& st,
             ss.coherence(L.na);
             const float4* Np = S.mesh_nodes + 2 * (size_t)L.na;   // child pair: 64 contiguous bytes
             float4 a0 = Np[0], a1 = Np[1], b0 = Np[2], b1 = Np[3];
-            IntersectBoxPair(L.O, L.Y, L.Time, a0, a1, b0, b1, TA, TB);
+            IntersectBoxPair(L.O, L.V, L.Y, L.Time, a0, a1, b0, b1, L.exact, TA, TB);
             aw0 = __float_as_uint(a0.w), aw1 = __float_as_uint(a1.w);
             bw0 = __float_as_uint(b0.w), bw1 = __float_as_uint(b1.w);
 #if PT_TWO_LEVEL
@@ -487,7 +490,7 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP, SE>& st,
                 pair = nw0;
                 const float4* Cp = S.mesh_nodes + 2 * (size_t)nw0;
                 float4 c0 = Cp[0], c1 = Cp[1], c2 = Cp[2], c3 = Cp[3];
-                IntersectBoxPair(L.O, L.Y, L.Time, c0, c1, c2, c3, TA, TB);
+                IntersectBoxPair(L.O, L.V, L.Y, L.Time, c0, c1, c2, c3, L.exact, TA, TB);
                 aw0 = __float_as_uint(c0.w), aw1 = __float_as_uint(c1.w);
                 bw0 = __float_as_uint(c2.w), bw1 = __float_as_uint(c3.w);
             }
@@ -548,7 +551,7 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP, SE>& st,
             const float4* Np = S.mesh_nodes + 2 * (size_t)Index;   // child pair: 64 contiguous bytes
             float4 a0 = Np[0], a1 = Np[1], b0 = Np[2], b1 = Np[3];
             float TA, TB;
-            IntersectBoxPair(L.O, L.Y, L.Time, a0, a1, b0, b1, TA, TB);
+            IntersectBoxPair(L.O, L.V, L.Y, L.Time, a0, a1, b0, b1, L.exact, TA, TB);
             // The reference's three-way decision (scene.glsl.inc:366-392) as
             // selects: B strictly closer -> continue with B, set A aside if
             // hit; otherwise continue with A if hit, setting B aside if it

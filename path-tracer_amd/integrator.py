@@ -53,7 +53,7 @@ class Device:
         _check(N.hip_lib().ptSynchronize(self._h), "ptSynchronize")
 
     def set_profiling(self, enable: bool, period: int = 1):
-        """Kernel timing with HIP events; period > 1 times every period-th Run only."""
+        """Kernel timing with HIP events; period > 1 times every period-th round only."""
         _check(N.hip_lib().ptSetProfiling(self._h, int(enable)), "ptSetProfiling")
         _check(N.hip_lib().ptSetProfilingPeriod(self._h, int(period)), "ptSetProfilingPeriod")
 
@@ -238,6 +238,15 @@ class BasicRenderer:
 
     def run(self, rounds: int = 1):
         _check(N.hip_lib().ptRunBasicRenderer(self.device.handle, self._h, int(rounds)), "ptRunBasicRenderer")
+
+    def render_frame(self, target_samples: int, max_rounds: int = 1 << 30):
+        """Benchmark-mode frame (ptRenderFrame): Reset,
+        Run(2), then Run(1) rounds until target_samples paths completed since
+        the Reset.  Blocks; returns (rounds, samples)."""
+        rounds, samples = C.c_uint32(0), C.c_uint64(0)
+        _check(N.hip_lib().ptRenderFrame(self.device.handle, self._h, int(target_samples), int(max_rounds),
+                                         C.byref(rounds), C.byref(samples)), "ptRenderFrame")
+        return int(rounds.value), int(samples.value)
 
     def stats(self):
         """(rays traced, paths completed) since the last Reset (ptGetStats)."""

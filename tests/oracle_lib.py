@@ -34,6 +34,10 @@ def lib():
         L.oracle_params.restype = vp
         L.oracle_params.argtypes = [vp]
         L.oracle_set_openpbr.argtypes = [vp, C.c_int]
+        L.oracle_set_slab_division.argtypes = [C.c_int]
+        L.oracle_slab_division.restype = C.c_int
+        L.oracle_intersect_bounding_box.restype = f32
+        L.oracle_intersect_bounding_box.argtypes = [fptr, fptr, f32, fptr, fptr]
         L.oracle_reset.argtypes = [vp]
         L.oracle_run.argtypes = [vp, u32]
         L.oracle_read_accum.argtypes = [vp, fptr]
@@ -58,6 +62,31 @@ def lib():
         L.oracle_preview.argtypes = [vp, vp, fptr, vp, C.POINTER(C.c_uint32)]
         _lib = L
     return _lib
+
+
+class slab_division:
+    """Context manager: the oracle's slab-test division convention inside the
+    block ("ieee": correctly rounded (Min-O)/V, the default and the HIP
+    kernels' convention; "rcp": RN((Min-O)*RN(1/V)), measurement only)."""
+
+    def __init__(self, mode):
+        assert mode in ("ieee", "rcp")
+        self.mode = mode
+
+    def __enter__(self):
+        self.prev = lib().oracle_slab_division()
+        lib().oracle_set_slab_division(1 if self.mode == "ieee" else 0)
+        return self
+
+    def __exit__(self, *exc):
+        lib().oracle_set_slab_division(self.prev)
+
+
+def intersect_bounding_box(origin, velocity, reach, mn, mx):
+    """The oracle's slab test (common.glsl.inc:153-185) in the current convention."""
+    a = [np.ascontiguousarray(x, dtype=np.float32) for x in (origin, velocity, mn, mx)]
+    p = [x.ctypes.data_as(C.POINTER(C.c_float)) for x in a]
+    return float(lib().oracle_intersect_bounding_box(p[0], p[1], float(reach), p[2], p[3]))
 
 
 class OracleRenderer:

@@ -1,24 +1,31 @@
-"""Writes profiles/traffic.json (read by bench.py) from a committed PMC summary.
+"""Writes one config's entry of profiles/traffic.json (read by bench.py:
+roofline.traffic and limiter of that config's line) from a committed PMC
+summary.
 
-usage: python tools/update_traffic.py profiles/<run>   (expects pmc_summary.json)
+usage: python tools/update_traffic.py CONFIG profiles/<run> ["command"]
+       (profiles/<run>/pmc_summary.json from profiles/pmc_summary.py)
 """
 import json
 import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-run = Path(sys.argv[1])
+config, run = sys.argv[1], Path(sys.argv[2])
+command = sys.argv[3] if len(sys.argv) > 3 else f"tools/gpu_profile.sh (bench.py --config {config}, N=1)"
 s = json.loads((ROOT / run / "pmc_summary.json").read_text())
-out = {"profile": str(run), "command": "tools/gpu_profile.sh (bench.py --gpus 1 --steps 20 --warmup 5: C3 1920x1080, N=1)", "kernels": {}, "issue": {}}
+entry = {"profile": str(run), "command": command, "kernels": {}, "issue": {}}
 for k in ("extend", "raygen", "shade", "round"):
     if k not in s:
         continue
-    out["kernels"][k] = {x: int(s[k][x]) for x in ("hbm_bytes", "hbm_read_bytes", "hbm_write_bytes") if x in s[k]}
+    entry["kernels"][k] = {x: int(s[k][x]) for x in ("hbm_bytes", "hbm_read_bytes", "hbm_write_bytes") if x in s[k]}
     iss = {x: s[k][x] for x in ("valu_issue_frac", "valu_active_lanes") if x in s[k]}
     for x in ("SQ_INSTS_VALU", "SQ_INSTS_SALU"):
         if x in s[k]:
             iss[x.lower()] = int(s[k][x])
     if iss:
-        out["issue"][k] = iss
-(ROOT / "profiles" / "traffic.json").write_text(json.dumps(out, indent=1) + "\n")
-print(json.dumps(out, indent=1))
+        entry["issue"][k] = iss
+path = ROOT / "profiles" / "traffic.json"
+d = json.loads(path.read_text()) if path.exists() else {}
+d.setdefault("configs", {})[str(config)] = entry
+path.write_text(json.dumps(d, indent=1) + "\n")
+print(json.dumps(entry, indent=1))
