@@ -1406,7 +1406,9 @@ int ptCommReduceSampleBuffer(pt_device* d, pt_comm* c, pt_sample_buffer* b, int 
                  "ptCommReduceSampleBufferInto)", c->nranks);
         return -1;
     }
-    if (b->nranks > 1 && ((int)b->nranks != c->nranks || (int)b->rank != c->rank)) {
+    // (A one-rank communicator sums nothing across ranks; it may reduce any
+    // partition -- the zeroing alone is then observable.)
+    if (c->nranks > 1 && b->nranks > 1 && ((int)b->nranks != c->nranks || (int)b->rank != c->rank)) {
         SetError("sample buffer partition %u/%u does not match communicator rank %d of %d", b->rank, b->nranks,
                  c->rank, c->nranks);
         return -1;

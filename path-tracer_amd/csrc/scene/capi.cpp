@@ -6,6 +6,8 @@
 #include "../../../include/pt_scene.h"
 
 #include <cstring>
+#include <exception>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -18,6 +20,24 @@ entity* E(pts_entity* e) { return reinterpret_cast<entity*>(e); }
 material* M(pts_material* m) { return reinterpret_cast<material*>(m); }
 texture* T(pts_texture* t) { return reinterpret_cast<texture*>(t); }
 mesh* Me(pts_mesh* m) { return reinterpret_cast<mesh*>(m); }
+
+// No exception crosses the C ABI: an entry point that parses files or
+// allocates from caller-given sizes runs under Guard, which turns
+// std::bad_alloc (or any other exception) into the error return.
+template <class R, class F>
+R Guard(R fail, const char* what, F&& f)
+{
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        g_err = std::string(what) + ": out of memory";
+    } catch (const std::exception& e) {
+        g_err = std::string(what) + ": " + e.what();
+    } catch (...) {
+        g_err = std::string(what) + ": unknown exception";
+    }
+    return fail;
+}
 }  // namespace
 
 extern "C" {
@@ -190,9 +210,11 @@ pts_texture* ptsCreateCheckerTexture(pts_scene* s, const char* name, int type, c
 pts_texture* ptsCreateTexture(pts_scene* s, const char* name, int type, uint32_t w, uint32_t h, const float* rgba, int nearest)
 {
     if (!rgba || w == 0 || h == 0) { g_err = "bad texture"; return nullptr; }
-    texture* t = CreateTexture(S(s), name, (uint32_t)type, w, h, rgba);
-    t->EnableNearestFiltering = nearest != 0;
-    return reinterpret_cast<pts_texture*>(t);
+    return Guard<pts_texture*>(nullptr, "CreateTexture", [&] {
+        texture* t = CreateTexture(S(s), name, (uint32_t)type, w, h, rgba);
+        t->EnableNearestFiltering = nearest != 0;
+        return reinterpret_cast<pts_texture*>(t);
+    });
 }
 
 pts_mesh* ptsCreateMesh(pts_scene* s, const char* name, uint32_t nv, const float* pos, const float* nrm, const float* uv,
@@ -201,7 +223,9 @@ pts_mesh* ptsCreateMesh(pts_scene* s, const char* name, uint32_t nv, const float
     if (!pos || !idx || nv == 0 || nf == 0) { g_err = "bad mesh"; return nullptr; }
     for (uint32_t i = 0; i < 3 * nf; i++)
         if (idx[i] >= nv) { g_err = "mesh index out of range"; return nullptr; }
-    return reinterpret_cast<pts_mesh*>(CreateMesh(S(s), name, nv, pos, nrm, uv, nf, idx));
+    return Guard<pts_mesh*>(nullptr, "CreateMesh", [&] {
+        return reinterpret_cast<pts_mesh*>(CreateMesh(S(s), name, nv, pos, nrm, uv, nf, idx));
+    });
 }
 
 uint32_t ptsMeshDepth(pts_mesh* m) { return Me(m)->Depth; }
@@ -221,22 +245,26 @@ void ptsDefaultLoadModelOptions(pts_load_model_options* o)
 
 int ptsLoadImageRGBA8(const char* path, uint32_t* w, uint32_t* h, uint8_t* rgba)
 {
-    int W = 0, H = 0;
-    std::vector<uint8_t> px;
-    std::string err;
-    if (!path || !LoadImageRGBA8(path, W, H, px, err)) { g_err = err.empty() ? "bad path" : err; return -1; }
-    if (w) *w = (uint32_t)W;
-    if (h) *h = (uint32_t)H;
-    if (rgba) std::memcpy(rgba, px.data(), px.size());
-    return 0;
+    return Guard(-1, "LoadImage", [&] {
+        int W = 0, H = 0;
+        std::vector<uint8_t> px;
+        std::string err;
+        if (!path || !LoadImageRGBA8(path, W, H, px, err)) { g_err = err.empty() ? "bad path" : err; return -1; }
+        if (w) *w = (uint32_t)W;
+        if (h) *h = (uint32_t)H;
+        if (rgba) std::memcpy(rgba, px.data(), px.size());
+        return 0;
+    });
 }
 
 pts_texture* ptsLoadTexture(pts_scene* s, const char* path, int type, const char* name)
 {
-    std::string err;
-    texture* t = LoadTexture(S(s), path, (uint32_t)type, name, &err);
-    if (!t) g_err = "LoadTexture: " + err;
-    return reinterpret_cast<pts_texture*>(t);
+    return Guard<pts_texture*>(nullptr, "LoadTexture", [&] {
+        std::string err;
+        texture* t = LoadTexture(S(s), path, (uint32_t)type, name, &err);
+        if (!t) g_err = "LoadTexture: " + err;
+        return reinterpret_cast<pts_texture*>(t);
+    });
 }
 
 pts_prefab* ptsLoadModelAsPrefab(pts_scene* s, const char* path, const pts_load_model_options* o)
@@ -253,27 +281,33 @@ pts_prefab* ptsLoadModelAsPrefab(pts_scene* s, const char* path, const pts_load_
         for (int i = 0; i < 9; i++) opt.TextureCoordinateTransform[i] = o->texcoord_transform[i];
         opt.OpenPBRAsDiffuse = o->openpbr_as_diffuse != 0;
     }
-    std::string err;
-    prefab* p = LoadModelAsPrefab(S(s), path, &opt, &err);
-    if (!p) g_err = "LoadModelAsPrefab: " + err;
-    return reinterpret_cast<pts_prefab*>(p);
+    return Guard<pts_prefab*>(nullptr, "LoadModelAsPrefab", [&] {
+        std::string err;
+        prefab* p = LoadModelAsPrefab(S(s), path, &opt, &err);
+        if (!p) g_err = "LoadModelAsPrefab: " + err;
+        return reinterpret_cast<pts_prefab*>(p);
+    });
 }
 
 pts_scene* ptsLoadScene(const char* path)
 {
     if (!path) { g_err = "LoadScene: null path"; return nullptr; }
-    std::string err;
-    scene* sc = LoadScene(path, &err);
-    if (!sc) g_err = "LoadScene: " + err;
-    return reinterpret_cast<pts_scene*>(sc);
+    return Guard<pts_scene*>(nullptr, "LoadScene", [&] {
+        std::string err;
+        scene* sc = LoadScene(path, &err);
+        if (!sc) g_err = "LoadScene: " + err;
+        return reinterpret_cast<pts_scene*>(sc);
+    });
 }
 
 int ptsSaveScene(pts_scene* s, const char* path)
 {
     if (!s || !path) { g_err = "SaveScene: null argument"; return -1; }
-    std::string err;
-    if (!SaveScene(path, S(s), &err)) { g_err = "SaveScene: " + err; return -1; }
-    return 0;
+    return Guard(-1, "SaveScene", [&] {
+        std::string err;
+        if (!SaveScene(path, S(s), &err)) { g_err = "SaveScene: " + err; return -1; }
+        return 0;
+    });
 }
 
 uint32_t ptsSceneTextureCount(pts_scene* s) { return s ? (uint32_t)S(s)->Textures.size() : 0; }

@@ -106,6 +106,7 @@ bool DecodePNG(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_
                                : (depth == 8 || depth == 16);
     if (!channels || !depth_ok || interlace > 1) { err = "unsupported PNG format"; return false; }
     if (ctype == 3 && plte.empty()) { err = "PNG palette missing"; return false; }
+    if (!StbSizesValid({w, h, 4})) { err = "too large"; return false; }
     int bits_pp = channels * depth;
 
     // inflate
@@ -211,6 +212,10 @@ bool DecodeHDR(const std::vector<uint8_t>& f, int& W, int& H, std::vector<vec4>&
     l = line();
     int h = 0, w = 0;
     if (std::sscanf(l.c_str(), "-Y %d +X %d", &h, &w) != 2 || w <= 0 || h <= 0) { err = "unsupported HDR layout"; return false; }
+    if (w > (1 << 24) || h > (1 << 24) || !StbSizesValid({(uint64_t)w, (uint64_t)h, 4, sizeof(float)})) {
+        err = "too large";
+        return false;
+    }
     W = w;
     H = h;
     px.assign((size_t)w * h, vec4(0, 0, 0, 1));
@@ -284,6 +289,14 @@ bool DecodeTGA(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_
                            : !(bits == 15 || bits == 16 || bits == 24 || bits == 32)) {
         err = "unsupported TGA pixel format";
         return false;
+    }
+    {
+        // stbi__tga_get_comp: the source components (palette entries for a
+        // colour-mapped image) -> stb's size guard.
+        const uint32_t eb = mapped ? cmbits : bits;
+        const uint64_t comp = base == 3 ? (bits == 16 ? 2 : 1) : (eb == 32 ? 4 : 3);
+        if (!StbSizesValid({w, h, comp})) { err = "too large"; return false; }
+        if (!StbSizesValid({4, w, h})) { err = "outofmem"; return false; }   // the RGBA8 output
     }
     size_t pos = 18 + idlen;
     // A pixel (or palette entry) of `b` bits -> RGBA8; grey when `grey`.
@@ -398,6 +411,7 @@ bool DecodeBMP(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_
     bool top_down = h < 0;
     if (top_down) h = -h;
     if (w <= 0 || h <= 0 || w > (1 << 24) || h > (1 << 24)) { err = "bad BMP size"; return false; }
+    if (!StbSizesValid({4, (uint64_t)w, (uint64_t)h})) { err = "too large"; return false; }
     if (comp != 0 && comp != 3) { err = "unsupported BMP compression"; return false; }
     if (bpp != 1 && bpp != 4 && bpp != 8 && bpp != 16 && bpp != 24 && bpp != 32) { err = "unsupported BMP depth"; return false; }
     uint32_t mr = 0, mg = 0, mb = 0, ma = 0;
@@ -528,7 +542,11 @@ bool DecodePNM(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_
     if (overflow) { err = "PNM header integer overflow"; return false; }
     if (maxv > 65535) { err = "PNM: max value > 65535"; return false; }
     const int bytes = maxv > 255 ? 2 : 1;
-    if (w > (1 << 24) || h > (1 << 24)) { err = "PNM: too large"; return false; }
+    if (w > (1 << 24) || h > (1 << 24) || !StbSizesValid({(uint64_t)comp, (uint64_t)w, (uint64_t)h, (uint64_t)bytes}) ||
+        !StbSizesValid({4, (uint64_t)w, (uint64_t)h})) {
+        err = "PNM: too large";
+        return false;
+    }
     const size_t n = (size_t)w * h;
     if (f.size() - std::min(f.size(), r.pos) < n * comp * bytes) { err = "PNM file truncated"; return false; }
     const uint8_t* d = f.data() + r.pos;
@@ -566,7 +584,7 @@ bool DecodeGIF(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_
     const uint32_t gw = r.get16le(), gh = r.get16le();
     const uint32_t flags = r.get8(), bgindex = r.get8();
     r.get8();   // aspect ratio
-    if (gw > (1u << 24) || gh > (1u << 24)) { err = "GIF: too large"; return false; }
+    if (gw > (1u << 24) || gh > (1u << 24) || !StbSizesValid({4, gw, gh})) { err = "GIF: too large"; return false; }
     uint8_t pal[256][4] = {}, lpal[256][4] = {};   // B, G, R, A as stb stores them
     auto colortable = [&](uint8_t (*t)[4], int entries, int transp) {
         for (int i = 0; i < entries; i++) {
@@ -752,6 +770,7 @@ bool DecodePSD(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_
     if (channels > 16) { err = "PSD: unsupported channel count"; return false; }
     const int32_t h = (int32_t)get32be(), w = (int32_t)get32be();
     if (h > (1 << 24) || w > (1 << 24) || h <= 0 || w <= 0) { err = "PSD: bad size"; return false; }
+    if (!StbSizesValid({4, (uint64_t)w, (uint64_t)h})) { err = "PSD: too large"; return false; }
     const uint32_t depth = get16be();
     if (depth != 8 && depth != 16) { err = "PSD: bit depth is not 8 or 16"; return false; }
     if (get16be() != 3) { err = "PSD: not in RGB color mode"; return false; }
@@ -761,6 +780,13 @@ bool DecodePSD(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_
     const uint32_t compression = get16be();
     if (compression > 1) { err = "PSD: unknown compression"; return false; }
     const size_t n = (size_t)w * h;
+    if (!compression) {
+        const size_t need = n * (size_t)std::min(channels, 4) * (depth == 16 ? 2 : 1);
+        if (f.size() - std::min(f.size(), r.pos) < need) { err = "PSD: truncated image data"; return false; }
+    } else if (f.size() - std::min(f.size(), r.pos) < (size_t)h * channels * 2) {
+        err = "PSD: truncated RLE row counts";
+        return false;
+    }
     std::vector<uint8_t> out(4 * n);
     if (compression) {
         r.skip((size_t)h * channels * 2);   // per-row byte counts
@@ -836,6 +862,7 @@ bool DecodeLDR(const std::vector<uint8_t>& f, int& W, int& H, std::vector<uint8_
     if (DecodePNM(f, W, H, rgba8, err, pnm)) return true;
     if (pnm) return false;
     if (DecodeTGA(f, W, H, rgba8, err)) return true;
+    if (err == "too large" || err == "outofmem") return false;   // a TGA header stb would also reject by size
     err = "unsupported image format (JPEG, PNG, BMP, GIF, PSD, PNM, TGA, Radiance HDR)";
     return false;
 }
@@ -850,6 +877,8 @@ bool LoadImageFloat(const char* Path, int& Width, int& Height, std::vector<vec4>
     if (f.size() >= 2 && f[0] == '#' && f[1] == '?') return DecodeHDR(f, Width, Height, Pixels, Error);
     std::vector<uint8_t> rgba8;
     if (!DecodeLDR(f, Width, Height, rgba8, Error)) return false;
+    // stbi__ldr_to_hdr's float buffer (stbi__malloc_mad4(x, y, 4, sizeof(float))).
+    if (!StbSizesValid({(uint64_t)Width, (uint64_t)Height, 4, sizeof(float)})) { Error = "outofmem"; return false; }
     Pixels.resize((size_t)Width * Height);
     for (size_t i = 0; i < Pixels.size(); i++) {     // stbi__ldr_to_hdr: gamma 2.2 on colour, alpha linear
         const uint8_t* p = &rgba8[4 * i];

@@ -27,6 +27,7 @@
 // §2); tests/test_jpeg.py checks decoding against independent encodes.
 #include "image.hpp"
 
+#include <climits>
 #include <cstring>
 
 namespace pth {
@@ -310,6 +311,24 @@ bool decoder::Restart()
     return true;
 }
 
+// stb_image 2.29's corrupt-stream checks on the DC path (stbi__addints_valid,
+// stbi__mul2shorts_valid): the predictor sum must fit an int and the
+// dequantised (or point-transformed) DC value a short.
+static bool AddIntsValid(int a, int b)
+{
+    if ((a >= 0) != (b >= 0)) return true;
+    if (a < 0 && b < 0) return a >= INT_MIN - b;
+    return a <= INT_MAX - b;
+}
+
+static bool Mul2ShortsValid(int a, int b)
+{
+    if (b == 0 || b == -1) return true;
+    if ((a >= 0) == (b >= 0)) return a <= SHRT_MAX / b;
+    if (b < 0) return a <= SHRT_MIN / b;
+    return a >= SHRT_MIN / b;
+}
+
 bool decoder::BlockBaseline(int16_t* blk, int ci)
 {
     component& c = comp_[ci];
@@ -318,7 +337,9 @@ bool decoder::BlockBaseline(int16_t* blk, int ci)
     if (t < 0 || t > 15) return Fail("bad Huffman code (DC)");
     std::memset(blk, 0, 64 * sizeof(int16_t));
     int diff = t ? Receive(t) : 0;
+    if (!AddIntsValid(c.dc_pred, diff)) return Fail("bad delta");
     c.dc_pred += diff;
+    if (!Mul2ShortsValid(c.dc_pred, q[0])) return Fail("can't merge dc and ac");
     blk[0] = (int16_t)(c.dc_pred * q[0]);
     for (int k = 1; k < 64;) {
         int rs = Huff(ac_[c.ta]);
@@ -346,7 +367,10 @@ bool decoder::BlockDC(int16_t* blk, int ci)
         std::memset(blk, 0, 64 * sizeof(int16_t));
         int t = Huff(dc_[c.td]);
         if (t < 0 || t > 15) return Fail("bad Huffman code (DC)");
-        c.dc_pred += t ? Receive(t) : 0;
+        int diff = t ? Receive(t) : 0;
+        if (!AddIntsValid(c.dc_pred, diff)) return Fail("bad delta");
+        c.dc_pred += diff;
+        if (!Mul2ShortsValid(c.dc_pred, 1 << al_)) return Fail("can't merge dc and ac");
         blk[0] = (int16_t)(c.dc_pred * (1 << al_));
     } else if (Bit()) {
         blk[0] = (int16_t)(blk[0] + (1 << al_));
@@ -540,6 +564,9 @@ bool decoder::Frame(int m)
     ncomp_ = Byte();
     if (ncomp_ != 1 && ncomp_ != 3 && ncomp_ != 4) return Fail("bad JPEG component count");
     if (Lf != 8 + 3 * ncomp_) return Fail("bad SOF length");
+    if (!StbSizesValid({(uint64_t)width_, (uint64_t)height_, (uint64_t)ncomp_})) return Fail("too large");
+    // stbi_load's 4-component output buffer (stbi__malloc_mad3(4, x, y)).
+    if (!StbSizesValid({4, (uint64_t)width_, (uint64_t)height_})) return Fail("outofmem");
     rgb_ids_ = 0;
     for (int i = 0; i < ncomp_; i++) {
         component& c = comp_[i];

@@ -399,6 +399,21 @@ bool ReadCompressed(std::istream& In, void* Data, size_t Size)
     return Got == Size;
 }
 
+// Whether `bytes` of decompressed data can come out of what is left of the
+// stream: deflate expands at most ~1032:1, so a header count beyond that is
+// a corrupt file, rejected before anything is allocated from it.
+bool PlausibleInflated(std::istream& In, uint64_t bytes)
+{
+    std::streampos At = In.tellg();
+    if (At < 0) return false;
+    In.seekg(0, std::ios::end);
+    std::streampos End = In.tellg();
+    In.seekg(At);
+    if (End < At || !In) return false;
+    uint64_t Left = (uint64_t)(End - At);
+    return bytes <= 1100 * Left + 4096;
+}
+
 constexpr uint32_t MAGIC_TEXTURE = 0x54455820u;   // 'TEX '
 constexpr uint32_t MAGIC_MESH = 0x4D455348u;      // 'MESH'
 constexpr uint32_t MAGIC_SPECTRUM = 0x53504543u;  // 'SPEC'
@@ -657,6 +672,10 @@ struct serializer {
         if (!File || Header[0] != MAGIC_TEXTURE) { Error = "bad texture file for '" + T.Name + "'"; return false; }
         T.Width = Header[2];
         T.Height = Header[3];
+        if (!PlausibleInflated(File, (uint64_t)T.Width * T.Height * sizeof(vec4))) {
+            Error = "corrupt texture data for '" + T.Name + "'";
+            return false;
+        }
         T.Pixels.resize((size_t)T.Width * T.Height);
         if (!ReadCompressed(File, T.Pixels.data(), sizeof(vec4) * T.Pixels.size())) {
             Error = "corrupt texture data for '" + T.Name + "'";
@@ -747,6 +766,10 @@ struct serializer {
         uint32_t Header[4] = {0, 0, 0, 0};
         File.read(reinterpret_cast<char*>(Header), sizeof Header);
         if (!File || Header[0] != MAGIC_MESH) { Error = "bad mesh file for '" + M.Name + "'"; return false; }
+        if (!PlausibleInflated(File, (uint64_t)Header[2] * sizeof(mesh_face) + (uint64_t)Header[3] * sizeof(mesh_node))) {
+            Error = "corrupt mesh data for '" + M.Name + "'";
+            return false;
+        }
         M.Faces.resize(Header[2]);
         M.Nodes.resize(Header[3]);
         if (!ReadCompressed(File, M.Faces.data(), sizeof(mesh_face) * M.Faces.size()) ||
@@ -756,6 +779,10 @@ struct serializer {
         }
         uint64_t VertexCount = 0;
         File.read(reinterpret_cast<char*>(&VertexCount), sizeof VertexCount);
+        if (File && VertexCount < (1ull << 32) && !PlausibleInflated(File, VertexCount * sizeof(mesh_vertex))) {
+            Error = "corrupt vertex data for '" + M.Name + "'";
+            return false;
+        }
         if (File && VertexCount < (1ull << 32)) {
             M.Vertices.resize((size_t)VertexCount);
             if (!ReadCompressed(File, M.Vertices.data(), sizeof(mesh_vertex) * M.Vertices.size())) {

@@ -56,7 +56,7 @@ for S in "$@"; do
       (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$O/trace_c$CFG" -o run -- python3 "$R/bench.py" $(BENCH_ARGS) --no-cpu-baseline > "$O/trace_c$CFG.log" 2>&1)
       rc=$?; [ $rc -eq 0 ] || fail trace $rc
       cp "$(find "$O/trace_c$CFG" -name '*kernel_stats.csv' | head -1)" "$O/kernel_stats_c$CFG.csv"
-      tail -1 "$O/trace_c$CFG.log" > "$O/trace_bench_c$CFG.json"
+      grep "^{\"metric\"" "$O/trace_c$CFG.log" | tail -1 > "$O/trace_bench_c$CFG.json"
       python3 "$R/profiles/timed_region.py" "$(find "$O/trace_c$CFG" -name '*kernel_trace.csv' | head -1)" "$O/trace_bench_c$CFG.json" "$O/timed_region_c$CFG.json" || true
       cut -d, -f1-8 "$O/kernel_stats_c$CFG.csv" | head -8 ;;
     pmc)
