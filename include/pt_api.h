@@ -264,6 +264,12 @@ int ptExtendStats(pt_device* device, pt_basic_renderer* renderer, uint64_t out[P
  * POSITION (steps[q], q < width-rounded slot count; 0 where no ray). */
 int ptExtendStepCounts(pt_device* device, pt_basic_renderer* renderer, uint32_t* steps);
 
+/* Diagnostic, caller-given rays (the ptTraceRays inputs): the counters of
+ * ptExtendStats and, if steps != NULL, each ray's traversal step count. */
+int ptTraceRaysStats(pt_device* device, pt_scene* scene, uint32_t n, const float* origins,
+                     const uint32_t* packed_velocities, const float* durations,
+                     uint64_t out[PT_EXTEND_STATS_COUNT], uint32_t* steps);
+
 /* Per-kernel device time, measured with HIP events on the renderer stream. */
 int ptSetProfiling(pt_device* device, int enable);
 /* Time only the kernels of every period-th round (default 1; rounds counted

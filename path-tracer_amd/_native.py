@@ -236,6 +236,7 @@ HIP_API = {
     "ptSetBasicRendererFusedRounds": (_i32, [_vp, _i32]),
     "ptSetBasicRendererOpenPBR": (_i32, [_vp, _i32]),
     "ptGetStats": (_i32, [_vp, _vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "ptTraceRaysStats": (_i32, [_vp, _vp, _u32, _fptr, _u32ptr, _fptr, C.POINTER(C.c_uint64), _vp]),
     "ptRenderFrame": (_i32, [_vp, _vp, C.c_uint64, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
     "ptReadBasicRendererState": (_i32, [_vp, _vp, _vp]),
     "ptTraceRays": (_i32, [_vp, _vp, _u32, _fptr, _u32ptr, _fptr, _vp]),

@@ -1431,16 +1431,34 @@ static hipError_t LaunchExtend(const ptd::dscene& S, const Src& src, uint32_t n,
     return hipGetLastError();
 }
 
-template <int CAP, class E>
-static void LaunchExtendStats(const ptd::dscene& S, const ptd::ray_source_slots& src, uint32_t n, uint32_t* spill,
+template <int CAP, class E, class Src>
+static void LaunchExtendStats(const ptd::dscene& S, const Src& src, uint32_t n, uint32_t* spill,
                               unsigned long long* out, uint32_t* steps, hipStream_t st)
 {
     if (spill)
-        hipLaunchKernelGGL((ptd::extend_stats_kernel<ptd::ray_source_slots, true, CAP, E>), dim3(Blocks(n)), dim3(256),
+        hipLaunchKernelGGL((ptd::extend_stats_kernel<Src, true, CAP, E>), dim3(Blocks(n)), dim3(256),
                            0, st, S, src, n, spill, n, out, steps);
     else
-        hipLaunchKernelGGL((ptd::extend_stats_kernel<ptd::ray_source_slots, false, CAP, E>), dim3(Blocks(n)),
+        hipLaunchKernelGGL((ptd::extend_stats_kernel<Src, false, CAP, E>), dim3(Blocks(n)),
                            dim3(256), 0, st, S, src, n, spill, n, out, steps);
+}
+
+hipError_t pt_launch_trace_rays_stats(const ptd::dscene& S, uint32_t n, const float* origins, const uint32_t* vel,
+                                      const float* dur, float4* hit, float2* hc, uint32_t* spill,
+                                      unsigned long long* out, uint32_t* steps, hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    ptd::ray_source_arrays src{origins, vel, dur, hit, hc};
+    switch (pt_extend_variant()) {
+#define X(id, w, cap)                                                                                           \
+    case id:                                                                                                   \
+        if (S.stack16) LaunchExtendStats<cap, uint16_t>(S, src, n, spill, out, steps, st);                      \
+        else LaunchExtendStats<cap, uint32_t>(S, src, n, spill, out, steps, st);                                \
+        break;
+        PT_EXTEND_VARIANTS(X)
+#undef X
+    }
+    return hipGetLastError();
 }
 
 hipError_t pt_launch_extend_stats(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* spill,

@@ -107,6 +107,10 @@ hipError_t pt_launch_zero_unowned(float4* accum, uint32_t width, uint32_t height
 hipError_t pt_launch_atlas_tile(const float4* src, float4* dst, uint32_t w, uint32_t h, uint32_t layers, hipStream_t st);
 hipError_t pt_launch_rcp_check(unsigned long long* mismatches, hipStream_t st);
 hipError_t pt_launch_xdiv_check(uint64_t n, uint32_t seed, unsigned long long* mismatches, hipStream_t st);
+// Diagnostic: the traversal counters of ptExtendStats for caller-given rays.
+hipError_t pt_launch_trace_rays_stats(const ptd::dscene& S, uint32_t n, const float* origins, const uint32_t* vel,
+                                      const float* dur, float4* hit, float2* hc, uint32_t* spill,
+                                      unsigned long long* out, uint32_t* steps, hipStream_t st);
 hipError_t pt_launch_trace_rays(const ptd::dscene& S, uint32_t n, const float* origins, const uint32_t* vel,
                                 const float* dur, float4* hit, float2* hc, float4* rec, float2* uv, uint32_t* spill,
                                 hipStream_t st);

@@ -1249,6 +1249,50 @@ int ptTraceRays(pt_device* d, pt_scene* s, uint32_t n, const float* origins, con
     return 0;
 }
 
+// Diagnostic: ptExtendStats's traversal counters for caller-given rays (the
+// ptTraceRays inputs), plus each ray's step count (order-independent: a ray's
+// traversal does not depend on its neighbours).
+int ptTraceRaysStats(pt_device* d, pt_scene* s, uint32_t n, const float* origins, const uint32_t* vel,
+                     const float* dur, uint64_t out[PT_EXTEND_STATS_COUNT], uint32_t* steps)
+{
+    if (!d || !s || !out || (n && (!origins || !vel || !dur))) { SetError("null argument"); return -1; }
+    if (!s->valid) { SetError("scene has no valid packs"); return -1; }
+    for (int i = 0; i < PT_EXTEND_STATS_COUNT; i++) out[i] = 0;
+    if (n == 0) return 0;
+    PT_HIP(hipSetDevice(d->id));
+    bool spill = s->stack_needed > pt_extend_stack_cap();
+    dbuf<float> d_o, d_t;
+    dbuf<uint32_t> d_v, d_spill, d_steps;
+    dbuf<float4> d_hit;
+    dbuf<float2> d_hc;
+    dbuf<unsigned long long> d_out;
+    hipError_t e = hipSuccess;
+    unsigned long long h[PT_EXTEND_STATS_COUNT] = {};
+    do {
+        if ((e = d_o.upload(origins, (size_t)n * 3)) != hipSuccess) break;
+        if ((e = d_t.upload(dur, n)) != hipSuccess) break;
+        if ((e = d_v.upload(vel, n)) != hipSuccess) break;
+        if ((e = d_hit.alloc(n)) != hipSuccess || (e = d_hc.alloc(n)) != hipSuccess) break;
+        if ((e = d_out.alloc(PT_EXTEND_STATS_COUNT)) != hipSuccess) break;
+        if (steps && (e = d_steps.alloc(n)) != hipSuccess) break;
+        if (spill && (e = d_spill.alloc((size_t)(s->stack_needed - pt_extend_stack_cap()) * n)) != hipSuccess) break;
+        if ((e = hipMemsetAsync(d_out.ptr, 0, sizeof(h), d->stream)) != hipSuccess) break;
+        e = pt_launch_trace_rays_stats(s->d, n, d_o.ptr, d_v.ptr, d_t.ptr, d_hit.ptr, d_hc.ptr,
+                                       spill ? d_spill.ptr : nullptr, d_out.ptr, steps ? d_steps.ptr : nullptr,
+                                       d->stream);
+        if (e != hipSuccess) break;
+        if ((e = hipMemcpyAsync(h, d_out.ptr, sizeof(h), hipMemcpyDeviceToHost, d->stream)) != hipSuccess) break;
+        if (steps && (e = hipMemcpyAsync(steps, d_steps.ptr, (size_t)n * 4, hipMemcpyDeviceToHost, d->stream)) != hipSuccess)
+            break;
+        e = hipStreamSynchronize(d->stream);
+    } while (0);
+    d_o.release(); d_t.release(); d_v.release(); d_spill.release(); d_steps.release();
+    d_hit.release(); d_hc.release(); d_out.release();
+    if (e != hipSuccess) { SetError("ptTraceRaysStats: %s", hipGetErrorString(e)); return (int)e; }
+    for (int i = 0; i < PT_EXTEND_STATS_COUNT; i++) out[i] = h[i];
+    return 0;
+}
+
 int ptCheckFastDivision(pt_device* d, uint64_t n, uint32_t seed, uint64_t* mismatches)
 {
     if (!d || !mismatches) { SetError("null argument"); return -1; }

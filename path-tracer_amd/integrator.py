@@ -117,6 +117,22 @@ class DeviceScene:
                                        out.ctypes.data), "ptTraceRays")
         return out
 
+    def trace_rays_stats(self, origins: np.ndarray, packed_velocities: np.ndarray, durations: np.ndarray):
+        """Traversal counters (ptExtendStats keys) and per-ray step counts of a
+        ray batch (diagnostic, ptTraceRaysStats)."""
+        o = np.ascontiguousarray(origins, dtype=np.float32).reshape(-1, 3)
+        v = np.ascontiguousarray(packed_velocities, dtype=np.uint32).reshape(-1)
+        d = np.ascontiguousarray(durations, dtype=np.float32).reshape(-1)
+        out = (C.c_uint64 * 14)()
+        steps = np.zeros(len(v), dtype=np.uint32)
+        _check(N.hip_lib().ptTraceRaysStats(self.device.handle, self._h, len(v), N.fptr(o), N.u32ptr(v), N.fptr(d),
+                                            out, steps.ctypes.data), "ptTraceRaysStats")
+        keys = ("rays", "lane_steps", "wave_steps_x64", "internal_nodes", "blas_leaves", "faces", "pops",
+                "tlas_leaves", "waves")
+        stats = dict(zip(keys, (int(x) for x in out)))
+        stats["simd_efficiency"] = stats["lane_steps"] / max(stats["wave_steps_x64"], 1)
+        return stats, steps
+
     def close(self):
         if self._h:
             N.hip_lib().ptDestroyScene(self.device.handle, self._h)

@@ -53,7 +53,9 @@ def main():
     r.RenderFlags = info.render_flags
     r.PathTerminationProbability = info.termination_probability
     r.reset()
-    r.run(2 + rounds)
+    r.run(2)
+    for _ in range(rounds):
+        r.run(1)
     dev.synchronize()
     st = r.read_state().reshape(-1)
     y, x = np.divmod(np.arange(W * H), W)
@@ -104,8 +106,47 @@ def main():
         "block256_oct_morton": blockwise((oct_ << 30) | mo, 256),
         "slot_again": np.arange(n),
     }
-    reps = 3
     dur = np.full(n, 1048576.0, np.float32)
+    # Per-ray traversal steps (order-independent), for longest-first block
+    # permutations of every order: a block lives as long as its slowest ray's
+    # wave, so blocks sorted by their max step count, descending, emulate the
+    # production extend's longest-first tile dispatch (with perfect costs).
+    stats, steps = ds.trace_rays_stats(O, PV, dur)
+    print("slot-order stats", json.dumps(stats), flush=True)
+
+    def lpt(p):
+        st = steps[p]
+        nb = (n + 255) // 256
+        pad = np.zeros(nb * 256, np.int64)
+        pad[:n] = st
+        cost = pad.reshape(nb, 256).max(1)
+        blocks = np.argsort(-cost, kind="stable")
+        idx = (blocks[:, None] * 256 + np.arange(256)[None, :]).reshape(-1)
+        idx = idx[idx < n]
+        return p[idx]
+
+    def groupwise(key, g):
+        idx = np.arange(n)
+        return np.lexsort((key, idx // (256 * g)))
+
+    orders["group4_oct_morton"] = groupwise((oct_ << np.uint64(30)) | mo, 4)
+    orders["group16_oct_morton"] = groupwise((oct_ << np.uint64(30)) | mo, 16)
+    orders["group64_oct_morton"] = groupwise((oct_ << np.uint64(30)) | mo, 64)
+    for k in list(orders):
+        if k != "slot_again":
+            orders[k + "+lpt"] = lpt(orders[k])
+    # per-order SIMD efficiency (wave max vs mean steps) and wave-step totals
+    eff = {}
+    for k, p in orders.items():
+        st = steps[p].astype(np.int64)
+        nw = (n + 63) // 64
+        pad = np.zeros(nw * 64, np.int64)
+        pad[:n] = st
+        w = pad.reshape(nw, 64)
+        eff[k] = {"wave_steps": int(w.max(1).sum()), "simd_eff": round(float(st.sum() / max(w.max(1).sum() * 64, 1)), 4)}
+    (ROOT / "gpurun_out").mkdir(exist_ok=True)
+    (ROOT / "gpurun_out" / "exp_reorder_eff.json").write_text(json.dumps(eff, indent=1))
+    reps = 3
     ref = None
     log = []
     for name, p in orders.items():

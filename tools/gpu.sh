@@ -13,6 +13,8 @@
 #   env=NAME=V[,..]    environment for later steps (A/B variants)
 #   ab=NAME=V1/V2[/..] the bench step once per value of NAME (env A/B on one box)
 #   smoke              __graft_entry__.smoke()
+#   flow               bench.py --gpus 2 --one-gpu-flow-check (self-launched ranks on one GPU; RCCL refuses
+#                      two ranks on one device, so the exchange takes the gloo fallback), both shards
 set -u
 TAG=${1:?tag}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -77,6 +79,13 @@ TCP_TOTAL_CACHE_ACCESSES_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCC_READ_REQ_sum G
 PASSES
       python3 "$R/profiles/pmc_summary.py" "$O/pmc_summary_c$CFG.json" $(find "$O" -path "*pmc_c${CFG}_*" -name "*counter_collection.csv") > "$O/pmc_summary_c$CFG.txt"
       grep -E "^(extend|shade|round)" "$O/pmc_summary_c$CFG.txt" | cut -c1-300 ;;
+    flow)
+      for sh in samples bands; do
+        (cd "$R" && timeout -k 10 400 python3 bench.py --gpus 2 --one-gpu-flow-check --steps 2 --warmup 1 --spp 64 --config $CFG --shard $sh --no-cpu-baseline --no-steady > "$O/flow_$sh.log" 2>&1)
+        rc=$?; [ $rc -eq 0 ] || { tail -20 "$O/flow_$sh.log"; fail "flow $sh" $rc; }
+        grep '^{"metric"' "$O/flow_$sh.log" | tail -1 > "$O/flow_$sh.json"
+        python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('flow', sys.argv[2], d['n_gpus'], d['value'], d['config']['exchange'], d['config']['comm_ranks'], d['frame']['rounds_per_frame_rank0'])" "$O/flow_$sh.json" $sh
+      done ;;
     smoke)
       (cd "$R" && timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1)
       rc=$?; tail -2 "$O/smoke.log"; [ $rc -eq 0 ] || fail smoke $rc ;;
