@@ -289,8 +289,14 @@ def main():
 
     frames = []   # (rounds, samples) per timed frame
 
+    # A frame that has not reached its target after 64x the rounds the spp
+    # target needs at one completed path per slot and round is broken: stop.
+    max_rounds = 64 * spp + 64
+
     def frame(record):
-        rounds, samples = r.render_frame(target)
+        rounds, samples = r.render_frame(target, max_rounds)
+        if samples < target:
+            raise RuntimeError(f"frame stopped at {rounds} rounds with {samples} of {target} samples")
         frame_end_exchange()
         if record:
             frames.append((rounds, samples))

@@ -97,7 +97,8 @@ enum {
     PT_KERNEL_RESOLVE = 3,
     PT_KERNEL_PREVIEW = 4,
     PT_KERNEL_ROUND   = 5,   /* fused extend + shade of a small partition (one launch per round) */
-    PT_KERNEL_COUNT   = 6,
+    PT_KERNEL_SORT    = 6,   /* global ray sort before extend (scan + scatter) */
+    PT_KERNEL_COUNT   = 7,
 };
 
 /* resolve_parameters (src/integrator/integrator.hpp:12-48). */

@@ -655,6 +655,51 @@ PT_DEV void TileOrderStoreRay(const dslots& L, uint32_t s, bool valid, pt3 O, pt
     L.slotof[q] = (uint8_t)(s & 255u);
 }
 
+// --- Global ray sort ---------------------------------------------------------
+//
+// TileOrder sorts a tile's 256 new rays by direction octant; the global sort
+// orders ALL of a frame's rays by (octant, Morton cell of the origin in a
+// 16^3 grid over the scene's bounds) before each extend, so a wave traces
+// rays that start in the same region in the same octant wherever their
+// pixels are.  Measured on C3's settled rays (tools/exp_reorder.py,
+// profiles/r03_reorder): with longest-first block dispatch the traversal of
+// the sorted order takes 0.76x that of the tile-octant order (SIMD efficiency
+// 0.53 -> 0.67; per-ray step counts do not depend on the order, so the hits
+// are identical).  Path state stays per slot (pixel tiles); only the rays
+// move: raygen / shade write each new ray by slot with its key and count the
+// key; at the next round's start a scan turns the counts into bin offsets and
+// a scatter gives every slot its position (perm / gpos); extend traces
+// position q = the ray of slot perm[q]; shade reads slot s's hit at gpos[s].
+PT_DEV uint32_t MortonSpread3(uint32_t v)   // 3 bits -> every third bit
+{
+    v &= 7u;
+    return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4);
+}
+
+// Sort key (12 bits): direction octant, then the origin's cell of an 8^3 grid
+// over the TLAS root box in Morton order.  The root box bounds every shape
+// (a scene without shapes reads the zeroed placeholder node: every origin
+// lands in cell 0).  Key choice measured in tools/exp_gsort.py.
+PT_DEV uint32_t RayKey(const dscene& S, pt3 O, pt3 V)
+{
+    float4 a = S.shape_nodes[0], b = S.shape_nodes[1];
+    float sx = 8.0f / fmaxf(b.x - a.x, 1e-30f), sy = 8.0f / fmaxf(b.y - a.y, 1e-30f), sz = 8.0f / fmaxf(b.z - a.z, 1e-30f);
+    uint32_t cx = (uint32_t)fminf(fmaxf((O.x - a.x) * sx, 0.0f), 7.0f);
+    uint32_t cy = (uint32_t)fminf(fmaxf((O.y - a.y) * sy, 0.0f), 7.0f);
+    uint32_t cz = (uint32_t)fminf(fmaxf((O.z - a.z) * sz, 0.0f), 7.0f);
+    uint32_t oct = (V.x < 0.0f ? 1u : 0u) | (V.y < 0.0f ? 2u : 0u) | (V.z < 0.0f ? 4u : 0u);
+    return (oct << 9) | MortonSpread3(cx) | (MortonSpread3(cy) << 1) | (MortonSpread3(cz) << 2);
+}
+
+// A new ray of slot s in global-sort mode: stored by slot with its key (the
+// next round's sort pass counts and places it).
+PT_DEV void GlobalSortStoreRay(const dscene& S, const dslots& L, uint32_t s, bool valid, pt3 O, pt3 V)
+{
+    if (!valid) return;
+    L.ray[s] = make_float4(O.x, O.y, O.z, __uint_as_float(PackUnitVector(V)));
+    L.key[s] = (uint16_t)RayKey(S, O, V);
+}
+
 // GenerateNewPath (basic_scatter.glsl:7-42) + GenerateCameraRay (scene.glsl.inc:613-655)
 PT_DEV void GenerateNewPath(const dscene& S, const dslots& L, const dframe& F, const dparams& Pm, rng& G, uint32_t s,
                             uint32_t x, uint32_t y, pt3& RO, pt3& RV, bool act_none = false)
@@ -847,7 +892,8 @@ __global__ __launch_bounds__(256) void raygen_kernel(dscene S, dslots L, dframe 
         GenerateNewPath(S, L, F, Pm, G, s, x, y, O, V);
         F.accum[(size_t)y * F.width + x] = make_float4(0, 0, 0, 0);
     }
-    TileOrderStoreRay(L, s, valid, O, V, L.pos[s] & 255u);
+    if (L.gsort) GlobalSortStoreRay(S, L, s, valid, O, V);
+    else TileOrderStoreRay(L, s, valid, O, V, L.pos[s] & 255u);
 }
 
 // Ray sources of the extend kernel: the renderer's slots, or the arrays of
@@ -911,6 +957,50 @@ struct ray_source_arrays {
         hc[i] = make_float2(Ln.C.y, Ln.C.z);
     }
 };
+
+// Global ray sort: position q < *nvalid traces the ray of slot perm[q] and
+// leaves its hit and outcome class at q.
+struct ray_source_sorted {
+    dslots L;
+    dframe F;
+    PT_DEV bool load(uint32_t q, pt3& O, pt3& V, float& D) const
+    {
+        if (q >= *L.nvalid) return false;
+        float4 r = L.ray[L.perm[q]];
+        O = v3(r.x, r.y, r.z);
+        V = UnpackUnitVector(__float_as_uint(r.w));
+        D = PT_HIT_TIME_LIMIT;
+        return true;
+    }
+    PT_DEV void store(uint32_t q, const lane_state& Ln, bool vidx21) const
+    {
+        L.hit[q] = CompactHit(Ln, vidx21);
+        L.uv[q] = make_float2(Ln.C.y, Ln.C.z);
+    }
+    PT_DEV void outcome(uint32_t q, uint32_t cls, bool) const { L.cls[q] = (uint8_t)cls; }
+};
+
+// Diagnostics in global-sort mode (ptExtendStats): slot s's current ray,
+// traced without storing anything (the next Run's sort decides positions).
+struct ray_source_slot_rays {
+    dslots L;
+    dframe F;
+    PT_DEV bool load(uint32_t s, pt3& O, pt3& V, float& D) const
+    {
+        uint32_t x, y;
+        if (!SlotPixel(F, s, x, y)) return false;
+        float4 r = L.ray[s];
+        O = v3(r.x, r.y, r.z);
+        V = UnpackUnitVector(__float_as_uint(r.w));
+        D = PT_HIT_TIME_LIMIT;
+        return true;
+    }
+    PT_DEV void store(uint32_t, const lane_state&, bool) const {}
+    PT_DEV void outcome(uint32_t, uint32_t, bool) const {}
+};
+
+template <class Src>
+constexpr bool kRendererSource = std::is_same<Src, ray_source_slots>::value || std::is_same<Src, ray_source_sorted>::value;
 
 // Extend: one ray per thread, LaneStep run to completion.  (A persistent
 // variant with per-wave dynamic ray fetch was measured 1.6x slower on C3: the
@@ -983,7 +1073,7 @@ PT_DEV void ExtendTile(const dscene& S, const Src& src, uint32_t n, uint32_t* sp
     st.spill = spill + slot;
     st.stride = spill_stride;
     ExtendRay<SPILL, CAP, E>(S, src, st, slot);
-    if constexpr (std::is_same<Src, ray_source_slots>::value) {
+    if constexpr (kRendererSource<Src>) {
         if (timed && (threadIdx.x & 63u) == 0)
             src.L.tilecost[tile * 4 + (threadIdx.x >> 6)] = (uint32_t)(__builtin_amdgcn_s_memtime() - t0);
     }
@@ -999,7 +1089,7 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
     // kernel's tail holds short blocks; each wave records its own time.
     uint32_t tile = blockIdx.x;
     bool timed = false;
-    if constexpr (std::is_same<Src, ray_source_slots>::value) {
+    if constexpr (kRendererSource<Src>) {
         tile += src.L.tile_base;
         if (src.L.order) {
             tile = src.L.order[blockIdx.x];
@@ -1089,6 +1179,110 @@ __global__ __launch_bounds__(256) void zero_unowned_kernel(float4* accum, uint32
         if (((y >> 4) % nranks) == rank) continue;
         for (uint32_t x = blockIdx.x * 256 + threadIdx.x; x < width; x += gridDim.x * 256)
             accum[(size_t)y * width + x] = make_float4(0, 0, 0, 0);
+    }
+}
+
+constexpr uint32_t GS_CHUNK = 8192;   // slots per block of the count / scatter kernels
+constexpr uint32_t GS_THREADS = 1024; // (8 slots per thread; 16 waves per block hide the atomics' latency)
+
+PT_DEV uint32_t GsKey(const dslots& L, const dframe& F, uint32_t s)
+{
+    uint32_t x, y;
+    return SlotPixel(F, s, x, y) ? (uint32_t)L.key[s] : PT_GS_BINS;
+}
+
+// Exclusive prefix sums of the key bins' counts (one block of GS_THREADS):
+// cursor[b] = rays of smaller keys; cursor[PT_GS_BINS] = *nvalid = all
+// valid rays (slots outside the image follow); the counts cleared.
+PT_DEV void GsScan(const dslots& L, uint32_t* cursor)
+{
+    constexpr uint32_t PER = PT_GS_BINS / GS_THREADS;
+    __shared__ uint32_t wsum[GS_THREADS / 64];
+    const uint32_t t = threadIdx.x, b0 = t * PER;
+    uint32_t local[PER];
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < PER; i++) {
+        local[i] = L.hist[b0 + i];
+        sum += local[i];
+    }
+    uint32_t incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t v = (uint32_t)__shfl_up((int)incl, o, 64);
+        if ((t & 63u) >= (uint32_t)o) incl += v;
+    }
+    if ((t & 63u) == 63u) wsum[t >> 6] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t w = 0; w < (t >> 6); w++) before += wsum[w];
+    uint32_t run = before + incl - sum;
+#pragma unroll
+    for (uint32_t i = 0; i < PER; i++) {
+        cursor[b0 + i] = run;
+        run += local[i];
+        L.hist[b0 + i] = 0;
+    }
+    if (t == GS_THREADS - 1) { cursor[PT_GS_BINS] = run; *L.nvalid = run; }
+}
+
+// Global ray sort pass (before each extend), three launches over the key
+// bins (PT_GS_BINS + one for slots outside the image):
+//   gsort_count_kernel    per chunk of GS_CHUNK slots an LDS histogram of the
+//                         keys, one global add per nonzero bin;
+//   gsort_scan_kernel     the bins' exclusive prefix sums (GsScan);
+//   gsort_scatter_kernel  per chunk again: each nonzero bin reserves its range
+//                         with one global atomic, each slot takes the next
+//                         position of its bin's range (LDS atomic) and
+//                         records it (gpos) and itself there (perm).
+// (Copying the rays into sorted order instead of extend gathering them
+// through perm: scatter +8 us, shade +10 us, extend -6 us; not kept.)
+// Same-address global atomics per ray serialise badly (camera rays share one
+// key): every global atomic here is per (chunk, bin).
+__global__ __launch_bounds__(GS_THREADS) void gsort_count_kernel(dslots L, dframe F)
+{
+    __shared__ uint32_t cnt[PT_GS_BINS + 1];
+    for (uint32_t b = threadIdx.x; b <= PT_GS_BINS; b += GS_THREADS) cnt[b] = 0;
+    __syncthreads();
+    const uint32_t s0 = blockIdx.x * GS_CHUNK;
+#pragma unroll
+    for (uint32_t i = 0; i < GS_CHUNK / GS_THREADS; i++) {
+        uint32_t s = s0 + i * GS_THREADS + threadIdx.x;
+        if (s < L.n) atomicAdd(&cnt[GsKey(L, F, s)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < PT_GS_BINS; b += GS_THREADS)
+        if (uint32_t c = cnt[b]) atomicAdd(&L.hist[b], c);
+}
+
+__global__ __launch_bounds__(GS_THREADS) void gsort_scan_kernel(dslots L, uint32_t* cursor) { GsScan(L, cursor); }
+
+__global__ __launch_bounds__(GS_THREADS) void gsort_scatter_kernel(dslots L, dframe F, uint32_t* cursor)
+{
+    __shared__ uint32_t cnt[PT_GS_BINS + 1], base[PT_GS_BINS + 1];
+    for (uint32_t b = threadIdx.x; b <= PT_GS_BINS; b += GS_THREADS) cnt[b] = 0;
+    __syncthreads();
+    const uint32_t s0 = blockIdx.x * GS_CHUNK;
+    uint32_t k[GS_CHUNK / GS_THREADS];
+#pragma unroll
+    for (uint32_t i = 0; i < GS_CHUNK / GS_THREADS; i++) {
+        uint32_t s = s0 + i * GS_THREADS + threadIdx.x;
+        k[i] = s < L.n ? GsKey(L, F, s) : 0u;
+        if (s < L.n) atomicAdd(&cnt[k[i]], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b <= PT_GS_BINS; b += GS_THREADS) {
+        uint32_t c = cnt[b];
+        if (c) base[b] = atomicAdd(&cursor[b], c);
+        cnt[b] = 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t i = 0; i < GS_CHUNK / GS_THREADS; i++) {
+        uint32_t s = s0 + i * GS_THREADS + threadIdx.x;
+        if (s >= L.n) continue;
+        uint32_t q = base[k[i]] + atomicAdd(&cnt[k[i]], 1u);
+        L.gpos[s] = q;
+        if (k[i] < PT_GS_BINS) L.perm[q] = s;
     }
 }
 
@@ -1198,19 +1392,38 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
     // tile run the surface path or the escape path, mostly not both; path
     // state is read and written by slot (gathers within the tile's records).
     const uint32_t base = tile * 256;
+    uint32_t s, p16 = 0;
+    if (L.gsort) {
+        // Global ray sort: the tile's outcome classes come from the positions
+        // its rays were traced at (one gathered byte per slot); the class
+        // masks are built in LDS, then ShadeOrder as below, by slot.
+        __shared__ uint64_t gm[4 * PT_OUTCOME_CLASSES];
+        uint32_t c = L.cls[L.gpos[base | threadIdx.x]];
+        uint32_t w = threadIdx.x >> 6;
+#pragma unroll
+        for (uint32_t k = 0; k < PT_OUTCOME_CLASSES; k++) {
+            uint64_t b = __ballot(c == k);
+            if ((threadIdx.x & 63u) == 0) gm[4 * k + w] = b;
+        }
+        __syncthreads();
+        const uint32_t pq = S.mat_classes ? ShadePosition(gm, threadIdx.x)
+                                          : ShadePosition2(gm + 4 * (PT_OUTCOME_CLASSES - 1), threadIdx.x);
+        s = base | pq;
+    } else {
 #if PT_SHADE_ORDER
-    // The position is the ray's own (slotof inverts TileOrder's slot ->
-    // position map), so the ray / hit / uv records load from it directly,
-    // beside the slotof lookup instead of after a pos[s] lookup.
-    const uint64_t* om = L.outcome + (size_t)tile * (4 * PT_OUTCOME_CLASSES);
-    const uint32_t pq = S.mat_classes ? ShadePosition(om, threadIdx.x)
-                                      : ShadePosition2(om + 4 * (PT_OUTCOME_CLASSES - 1), threadIdx.x);
-    uint32_t s = base | L.slotof[base | pq];
-    const uint32_t p16 = pq << 8;   // RayPos(s, p16) == base | pq (shade -1 % vs gathering pos[s])
+        // The position is the ray's own (slotof inverts TileOrder's slot ->
+        // position map), so the ray / hit / uv records load from it directly,
+        // beside the slotof lookup instead of after a pos[s] lookup.
+        const uint64_t* om = L.outcome + (size_t)tile * (4 * PT_OUTCOME_CLASSES);
+        const uint32_t pq = S.mat_classes ? ShadePosition(om, threadIdx.x)
+                                          : ShadePosition2(om + 4 * (PT_OUTCOME_CLASSES - 1), threadIdx.x);
+        s = base | L.slotof[base | pq];
+        p16 = pq << 8;   // RayPos(s, p16) == base | pq (shade -1 % vs gathering pos[s])
 #else
-    uint32_t s = base | threadIdx.x;
-    uint32_t p16 = L.pos[s];
+        s = base | threadIdx.x;
+        p16 = L.pos[s];
 #endif
+    }
     uint32_t x, y;
     bool valid = SlotPixel(F, s, x, y);
     pt3 O = v3s(0), V = v3s(0);
@@ -1237,8 +1450,8 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
         // (Trace, scene.glsl.inc:535-608) are rebuilt here and go through the
         // same octahedral snorm16 quantisation as the reference's
         // StoreTraceHit / LoadTraceResult.
-        uint32_t q = RayPos(L, s, p16);
-        float4 r = L.ray[q];
+        uint32_t q = L.gsort ? L.gpos[s] : RayPos(L, s, p16);
+        float4 r = L.ray[L.gsort ? s : q];
         O = v3(r.x, r.y, r.z);
         V = UnpackUnitVector(__float_as_uint(r.w));
         float4 h = L.hit[q];
@@ -1281,7 +1494,8 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
     // updated by the wave's first lane (no atomics: a wave owns its word).
     uint64_t cm = __ballot(completed);
     if ((threadIdx.x & 63u) == 0) L.done[(base | threadIdx.x) >> 6] += (uint32_t)__popcll(cm);
-    TileOrderStoreRay(L, s, valid, O, V, p16 >> 8);
+    if (L.gsort) GlobalSortStoreRay(S, L, s, valid, O, V);
+    else TileOrderStoreRay(L, s, valid, O, V, p16 >> 8);
 }
 
 template <uint32_t MATS>
@@ -1466,16 +1680,31 @@ hipError_t pt_launch_extend_stats(const ptd::dscene& S, const ptd::dslots& L, co
 {
     if (L.n == 0) return hipSuccess;
     ptd::ray_source_slots src{L, F};
+    ptd::ray_source_slot_rays gsrc{L, F};
     // The same LDS stack capacity and entry width as the render kernel.
     switch (pt_extend_variant()) {
 #define X(id, w, cap)                                                                                           \
     case id:                                                                                                   \
-        if (S.stack16) LaunchExtendStats<cap, uint16_t>(S, src, L.n, spill, out, steps, st);                    \
+        if (L.gsort) {                                                                                         \
+            if (S.stack16) LaunchExtendStats<cap, uint16_t>(S, gsrc, L.n, spill, out, steps, st);              \
+            else LaunchExtendStats<cap, uint32_t>(S, gsrc, L.n, spill, out, steps, st);                        \
+        } else if (S.stack16) LaunchExtendStats<cap, uint16_t>(S, src, L.n, spill, out, steps, st);           \
         else LaunchExtendStats<cap, uint32_t>(S, src, L.n, spill, out, steps, st);                              \
         break;
         PT_EXTEND_VARIANTS(X)
 #undef X
     }
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_gsort(const ptd::dslots& L, const ptd::dframe& F, uint32_t* cursor, hipStream_t st)
+{
+    if (L.n == 0) return hipSuccess;
+    static_assert(PT_GS_BINS % ptd::GS_THREADS == 0, "scan: whole bins per thread");
+    const uint32_t chunks = (L.n + ptd::GS_CHUNK - 1) / ptd::GS_CHUNK;
+    hipLaunchKernelGGL(ptd::gsort_count_kernel, dim3(chunks), dim3(ptd::GS_THREADS), 0, st, L, F);
+    hipLaunchKernelGGL(ptd::gsort_scan_kernel, dim3(1), dim3(ptd::GS_THREADS), 0, st, L, cursor);
+    hipLaunchKernelGGL(ptd::gsort_scatter_kernel, dim3(chunks), dim3(ptd::GS_THREADS), 0, st, L, F, cursor);
     return hipGetLastError();
 }
 
@@ -1516,6 +1745,7 @@ hipError_t pt_launch_zero_unowned(float4* accum, uint32_t width, uint32_t height
 hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* spill,
                             hipStream_t st)
 {
+    if (L.gsort) return LaunchExtend(S, ptd::ray_source_sorted{L, F}, L.n, L.tile_count, spill, st);
     return LaunchExtend(S, ptd::ray_source_slots{L, F}, L.n, L.tile_count, spill, st);
 }
 

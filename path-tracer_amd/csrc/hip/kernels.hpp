@@ -38,6 +38,17 @@ struct dslots {
     uint32_t* order;    // extend's block -> tile map (longest previous extend first), or null
     uint32_t* done;     // per wave of 64 slots: paths completed by shade since the last Reset (ptGetStats)
     uint32_t* spill;    // traversal stack spill: (needed - LDS capacity) rows x n
+    // Global ray sort (gsort != 0, kernels.hip "Global ray sort"): extend
+    // traces the rays in key order over the whole frame instead of tile by
+    // tile.  `ray` is then indexed by slot, and:
+    uint32_t* perm;     // per position: the slot whose ray extend traces there
+    uint32_t* nvalid;   // positions [0, *nvalid) hold rays (slots inside the image)
+    uint32_t* gpos;     // per slot: position of its ray in the last extend
+    uint16_t* key;      // per slot: sort key of its current ray (RayKey, written by raygen / shade)
+    uint32_t* hist;     // per key bin: the frame's count (sort pass; cleared by the scan);
+                        // hist[PT_GS_BINS + 1]: the count kernel's block ticket
+    uint8_t* cls;       // per position: the traced ray's ShadeOrder outcome class
+    uint32_t gsort;
     uint32_t n;
     // The launch's tile range (a run group, runtime.hip): tiles
     // [tile_base, tile_base + tile_count); `order` then points at the group's
@@ -90,6 +101,10 @@ hipError_t pt_launch_resolve(const float4* accum, uint32_t n, float brightness, 
                              uint32_t* out8, hipStream_t st);
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
                            uint32_t scene_mats, hipStream_t st);
+// Global ray sort before an extend: key counts (hist), their exclusive prefix
+// sums (cursor, hist cleared), then every slot's position (gpos, perm).  PT_GS_BINS key bins + one for slots outside the image.
+constexpr uint32_t PT_GS_BINS = 4096;
+hipError_t pt_launch_gsort(const ptd::dslots& L, const ptd::dframe& F, uint32_t* cursor, hipStream_t st);
 hipError_t pt_launch_vertex_decode(const uint2* v, uint32_t n, float4* attr, float* vv, hipStream_t st);
 hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st);
 // Fused round (extend + shade per tile in one launch, round_kernel): the

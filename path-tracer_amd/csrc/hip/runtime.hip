@@ -160,6 +160,11 @@ struct pt_basic_renderer {
     dbuf<uint32_t> tilecost, order;     // longest-first tile order (extend -> tile_order -> extend)
     uint64_t order_tick = 0;            // rounds since creation (tile-order re-sort period)
     dbuf<uint32_t> done;                // per wave: completed paths since the last Reset (ptGetStats)
+    // Global ray sort (PT_GLOBAL_SORT, kernels.hip): per-position slot, per-slot
+    // position and key, key-bin counts and cursors, per-position outcome class.
+    dbuf<uint32_t> perm, nvalid, gpos, hist, cursor;
+    dbuf<uint16_t> key;
+    dbuf<uint8_t> cls;
     // Run groups: the tiles split into `groups` contiguous ranges, each
     // advanced round by round on its own stream, so a group's next round
     // starts while another group's extend is still draining its longest
@@ -740,6 +745,14 @@ static uint32_t RunGroups(uint32_t tiles, uint32_t cus)
     return std::max<uint32_t>(1u, std::min<uint32_t>(g, tiles));
 }
 
+// PT_GLOBAL_SORT=1: extend traces the frame's rays in global key order
+// (kernels.hip "Global ray sort") instead of tile by tile (TileOrder).
+static bool GlobalSortEnabled()
+{
+    const char* e = getenv("PT_GLOBAL_SORT");
+    return e && atoi(e) != 0;
+}
+
 // PT_TILE_ORDER=0: extend dispatches tiles in their natural order.
 static bool TileOrderEnabled()
 {
@@ -813,10 +826,34 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     r->slots.order = TileOrderEnabled() && ns ? r->order.ptr : nullptr;
     r->slots.done = r->done.ptr;
     r->slots.spill = nullptr;
+    r->slots.gsort = 0;
+    r->slots.perm = nullptr; r->slots.nvalid = nullptr; r->slots.gpos = nullptr; r->slots.key = nullptr;
+    r->slots.hist = nullptr;
+    r->slots.cls = nullptr;
     r->slots.n = ns;
     r->slots.tile_base = 0;
     r->slots.tile_count = ns / 256;
     r->groups = RunGroups(ns / 256, d->cu_count);
+    if (GlobalSortEnabled() && ns && r->groups == 1) {
+        const size_t nb = PT_GS_BINS + 1;
+        ok = r->perm.alloc(ns) == hipSuccess && r->nvalid.alloc(1) == hipSuccess &&
+             r->gpos.alloc(ns) == hipSuccess &&
+             r->key.alloc(ns) == hipSuccess && r->hist.alloc(nb) == hipSuccess && r->cursor.alloc(nb) == hipSuccess &&
+             r->cls.alloc(ns) == hipSuccess &&
+             hipMemset(r->perm.ptr, 0, (size_t)ns * 4) == hipSuccess &&
+             hipMemset(r->nvalid.ptr, 0, 4) == hipSuccess &&
+             hipMemset(r->gpos.ptr, 0, (size_t)ns * 4) == hipSuccess &&
+             hipMemset(r->key.ptr, 0, (size_t)ns * 2) == hipSuccess && hipMemset(r->hist.ptr, 0, nb * 4) == hipSuccess &&
+             hipMemset(r->cls.ptr, 0, ns) == hipSuccess;
+        r->slots.gsort = 1;
+        r->slots.perm = r->perm.ptr; r->slots.nvalid = r->nvalid.ptr; r->slots.gpos = r->gpos.ptr; r->slots.key = r->key.ptr;
+        r->slots.hist = r->hist.ptr; r->slots.cls = r->cls.ptr;
+        if (!ok) {
+            SetError("renderer global-sort allocation failed (%u slots)", ns);
+            ptDestroyBasicRenderer(d, r);
+            return nullptr;
+        }
+    }
     for (uint32_t g = 0; g < r->groups && r->groups > 1 && ok; g++)
         ok = hipStreamCreateWithFlags(&r->gstream[g], hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&r->gevent[g], hipEventDisableTiming) == hipSuccess;
@@ -847,6 +884,8 @@ void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
     r->tilecost.release(); r->order.release();
     r->done.release();
     r->spill.release();
+    r->perm.release(); r->nvalid.release(); r->gpos.release(); r->key.release(); r->hist.release(); r->cursor.release();
+    r->cls.release();
     for (uint32_t g = 0; g < pt_basic_renderer::MAX_GROUPS; g++) {
         if (r->gstream[g]) (void)hipStreamDestroy(r->gstream[g]);
         if (r->gevent[g]) (void)hipEventDestroy(r->gevent[g]);
@@ -893,7 +932,7 @@ static uint32_t ShadeMats(const pt_basic_renderer* r)
 static bool RoundFused(const pt_basic_renderer* r, const ptd::dslots& g)
 {
     const int mode = r->fused;
-    if (mode == 0 || g.spill || g.tile_count == 0) return false;
+    if (mode == 0 || g.spill || g.tile_count == 0 || g.gsort) return false;
     uint32_t cap = pt_round_capacity(ShadeMats(r), r->scene->d.stack16 != 0, r->dev->cu_count);
     if (cap == 0) return false;
     return mode == 2 || g.tile_count <= cap;
@@ -951,6 +990,12 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
                     if (int e = EndTimed(d, ep)) return e;
                     if (sort) PT_HIP(pt_launch_tile_order(gs[g], st[g]));
                     continue;
+                }
+                if (gs[g].gsort) {
+                    event_pair es{};
+                    if (int e = BeginTimed(d, PT_KERNEL_SORT, es, sampled, st[g])) return e;
+                    PT_HIP(pt_launch_gsort(gs[g], F, r->cursor.ptr, st[g]));
+                    if (int e = EndTimed(d, es)) return e;
                 }
                 if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled, st[g])) return e;
                 PT_HIP(pt_launch_extend(r->scene->d, gs[g], F, r->slots.spill, st[g]));
@@ -1079,6 +1124,8 @@ int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state*
     PT_HIP(hipMemcpy(lam.data(), r->lam.ptr, (size_t)n * 4, hipMemcpyDeviceToHost));
     PT_HIP(hipMemcpy(act.data(), r->act.ptr, (size_t)n * 8, hipMemcpyDeviceToHost));
     PT_HIP(hipMemcpy(pos.data(), r->pos.ptr, (size_t)n * 2, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> gpos(r->slots.gsort ? n : 0);
+    if (r->slots.gsort) PT_HIP(hipMemcpy(gpos.data(), r->gpos.ptr, (size_t)n * 4, hipMemcpyDeviceToHost));
     uint32_t W = r->buffer->width, H = r->buffer->height;
     auto bits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
     for (uint32_t s = 0; s < n; s++) {
@@ -1086,8 +1133,10 @@ int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state*
         uint32_t x = tx * 16 + (l & 15u), y = (r->rank + k * r->nranks) * 16 + (l >> 4);
         if (x >= W || y >= H) continue;
         pt_pixel_state& O = out[(size_t)y * W + x];
-        // Ray and hit records live at the slot's TileOrder positions.
+        // Ray and hit records live at the slot's TileOrder positions (global
+        // sort: the ray by slot, the hit at the slot's last extend position).
         uint32_t qr = (s & ~255u) | (pos[s] >> 8u), qh = (s & ~255u) | (pos[s] & 255u);
+        if (r->slots.gsort) { qr = s; qh = gpos[s]; }
         O.origin[0] = ray[qr].x; O.origin[1] = ray[qr].y; O.origin[2] = ray[qr].z;
         O.packed_velocity = bits(ray[qr].w);
         O.hit.time = hit[qh].x;

@@ -66,7 +66,7 @@ for S in "$@"; do
       while read -r P; do
         [ -z "$P" ] && continue
         i=$((i+1))
-        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d "$O/pmc_c${CFG}_$i" -o run -- python3 "$R/bench.py" --steps 1 --warmup 0 --config $CFG $EXTRA --no-cpu-baseline --no-steady > "$O/pmc_c${CFG}_$i.log" 2>&1)
+        (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d "$O/pmc_c${CFG}_$i" -o run -- python3 "$R/bench.py" --steps 1 --warmup 0 --spp 256 --config $CFG $EXTRA --no-cpu-baseline --no-steady > "$O/pmc_c${CFG}_$i.log" 2>&1)
         rc=$?; echo "pmc pass $i ($P) rc=$rc"; [ $rc -eq 0 ] || fail pmc $rc
       done <<'PASSES'
 FETCH_SIZE
