@@ -679,7 +679,11 @@ PT_DEV uint32_t MortonSpread3(uint32_t v)   // 3 bits -> every third bit
 // Sort key (12 bits): direction octant, then the origin's cell of an 8^3 grid
 // over the TLAS root box in Morton order.  The root box bounds every shape
 // (a scene without shapes reads the zeroed placeholder node: every origin
-// lands in cell 0).  Key choice measured in tools/exp_gsort.py.
+// lands in cell 0).  Key choice: tools/exp_gsort.py (profiles/r03_gsort).
+// Two direction bits more (14-bit keys, 16384 bins) made the traversal
+// faster in that experiment (0.80x vs 0.89x of the tile-order layout) but
+// in the renderer extend only 0.88x, while the count / scan / scatter pass
+// grew from 34 to 52 us; not kept.
 PT_DEV uint32_t RayKey(const dscene& S, pt3 O, pt3 V)
 {
     float4 a = S.shape_nodes[0], b = S.shape_nodes[1];
@@ -1258,7 +1262,9 @@ __global__ __launch_bounds__(GS_THREADS) void gsort_scan_kernel(dslots L, uint32
 
 __global__ __launch_bounds__(GS_THREADS) void gsort_scatter_kernel(dslots L, dframe F, uint32_t* cursor)
 {
-    __shared__ uint32_t cnt[PT_GS_BINS + 1], base[PT_GS_BINS + 1];
+    // One LDS word per bin: the chunk's count, then (after the reservation)
+    // the next free position of the chunk's range in that bin.
+    __shared__ uint32_t cnt[PT_GS_BINS + 1];
     for (uint32_t b = threadIdx.x; b <= PT_GS_BINS; b += GS_THREADS) cnt[b] = 0;
     __syncthreads();
     const uint32_t s0 = blockIdx.x * GS_CHUNK;
@@ -1270,17 +1276,14 @@ __global__ __launch_bounds__(GS_THREADS) void gsort_scatter_kernel(dslots L, dfr
         if (s < L.n) atomicAdd(&cnt[k[i]], 1u);
     }
     __syncthreads();
-    for (uint32_t b = threadIdx.x; b <= PT_GS_BINS; b += GS_THREADS) {
-        uint32_t c = cnt[b];
-        if (c) base[b] = atomicAdd(&cursor[b], c);
-        cnt[b] = 0;
-    }
+    for (uint32_t b = threadIdx.x; b <= PT_GS_BINS; b += GS_THREADS)
+        if (uint32_t c = cnt[b]) cnt[b] = atomicAdd(&cursor[b], c);
     __syncthreads();
 #pragma unroll
     for (uint32_t i = 0; i < GS_CHUNK / GS_THREADS; i++) {
         uint32_t s = s0 + i * GS_THREADS + threadIdx.x;
         if (s >= L.n) continue;
-        uint32_t q = base[k[i]] + atomicAdd(&cnt[k[i]], 1u);
+        uint32_t q = atomicAdd(&cnt[k[i]], 1u);
         L.gpos[s] = q;
         if (k[i] < PT_GS_BINS) L.perm[q] = s;
     }

@@ -134,6 +134,22 @@ def main():
         wm = w.reshape(-1, 64).max(1)
         eff[name] = {"simd_eff": round(float(steps[1].sum() / (wm.sum() * 64)), 4),
                      "stale_cost_corr": round(float(np.corrcoef(block_cost(steps[0][pa]), block_cost(steps[1][pb]))[0, 1]), 3)}
+    # Baseline: the production layout (TileOrder: octant sort inside each
+    # 256-slot tile) with the stale longest-first order of the same tiles.
+    octs = [K[i]["oct_cell8"] >> np.uint64(9) for i in range(2)]
+    idx = np.arange(n)
+    ta = np.lexsort((octs[0], idx // 256))
+    tb = np.lexsort((octs[1], idx // 256))
+    orders["tileorder|stale"] = by_blocks(tb, block_cost(steps[0][ta]))
+    orders["tileorder|perfect"] = by_blocks(tb, block_cost(steps[1][tb]))
+    # Sorts inside groups of G tiles (one LDS counting sort per group, no
+    # global pass), with the stale order of the groups' blocks.
+    for G in (16, 32, 64):
+        for name in ("oct_cell8", "oct_cell8_dir4"):
+            ga = np.lexsort((K[0][name], idx // (256 * G)))
+            gb = np.lexsort((K[1][name], idx // (256 * G)))
+            orders[f"group{G}_{name}|stale"] = by_blocks(gb, block_cost(steps[0][ga]))
+            orders[f"group{G}_{name}|nolpt"] = gb
     orders["slot"] = np.arange(n)
     print(json.dumps(eff, indent=1), flush=True)
     O, PV = rays[1]
