@@ -668,8 +668,8 @@ PT_DEV void TileOrderStoreRay(const dslots& L, uint32_t s, bool valid, pt3 O, pt
 // are identical).  Path state stays per slot (pixel tiles); only the rays
 // move: raygen / shade write each new ray by slot with its key and count the
 // key; at the next round's start a scan turns the counts into bin offsets and
-// a scatter gives every slot its position (perm / gpos); extend traces
-// position q = the ray of slot perm[q]; shade reads slot s's hit at gpos[s].
+// a scatter gives every position its slot (perm); extend traces position q
+// = the ray of slot perm[q] and stores the hit by slot, where shade reads it.
 PT_DEV uint32_t MortonSpread3(uint32_t v)   // 3 bits -> every third bit
 {
     v &= 7u;
@@ -696,7 +696,12 @@ PT_DEV uint32_t RayKey(const dscene& S, pt3 O, pt3 V)
 }
 
 // A new ray of slot s in global-sort mode: stored by slot with its key (the
-// next round's sort pass counts and places it).
+// next round's sort pass counts and places it).  (Counting here instead, a
+// ballot per distinct key of the wave and one returning atomic per group
+// into key counters split over 8 tile classes, removed the count kernel
+// (9.8 us) but cost shade 13 us and raygen 48 us on C3: the camera rays'
+// few keys still queue their atomics; a single counter per key cost shade
+// 114 us.)
 PT_DEV void GlobalSortStoreRay(const dscene& S, const dslots& L, uint32_t s, bool valid, pt3 O, pt3 V)
 {
     if (!valid) return;
@@ -976,12 +981,16 @@ struct ray_source_sorted {
         D = PT_HIT_TIME_LIMIT;
         return true;
     }
+    // The hit and its outcome class go to the ray's SLOT (perm[q], re-read:
+    // an L1 hit), so shade reads them coalesced; extend's scattered stores
+    // cost less than shade's scattered loads did.
     PT_DEV void store(uint32_t q, const lane_state& Ln, bool vidx21) const
     {
-        L.hit[q] = CompactHit(Ln, vidx21);
-        L.uv[q] = make_float2(Ln.C.y, Ln.C.z);
+        uint32_t s = L.perm[q];
+        L.hit[s] = CompactHit(Ln, vidx21);
+        L.uv[s] = make_float2(Ln.C.y, Ln.C.z);
     }
-    PT_DEV void outcome(uint32_t q, uint32_t cls, bool) const { L.cls[q] = (uint8_t)cls; }
+    PT_DEV void outcome(uint32_t q, uint32_t cls, bool) const { L.cls[L.perm[q]] = (uint8_t)cls; }
 };
 
 // Diagnostics in global-sort mode (ptExtendStats): slot s's current ray,
@@ -1093,7 +1102,11 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
     // kernel's tail holds short blocks; each wave records its own time.
     uint32_t tile = blockIdx.x;
     bool timed = false;
-    if constexpr (kRendererSource<Src>) {
+    if constexpr (std::is_same<Src, ray_source_sorted>::value) {
+        // Global sort: block b traces positions [256b, 256b + 256), which the
+        // sort pass filled longest-first; the wave times feed the next scan.
+        timed = src.L.gcost != 0;
+    } else if constexpr (kRendererSource<Src>) {
         tile += src.L.tile_base;
         if (src.L.order) {
             tile = src.L.order[blockIdx.x];
@@ -1195,49 +1208,173 @@ PT_DEV uint32_t GsKey(const dslots& L, const dframe& F, uint32_t s)
     return SlotPixel(F, s, x, y) ? (uint32_t)L.key[s] : PT_GS_BINS;
 }
 
-// Exclusive prefix sums of the key bins' counts (one block of GS_THREADS):
-// cursor[b] = rays of smaller keys; cursor[PT_GS_BINS] = *nvalid = all
-// valid rays (slots outside the image follow); the counts cleared.
-PT_DEV void GsScan(const dslots& L, uint32_t* cursor)
+// Block-wide (GS_THREADS) exclusive scan: returns the sum of v over the
+// threads before this one; *total (every thread) = the sum over all.
+template <class T>
+PT_DEV T GsBlockScan(T v, T* wsum, T* total)
 {
-    constexpr uint32_t PER = PT_GS_BINS / GS_THREADS;
-    __shared__ uint32_t wsum[GS_THREADS / 64];
-    const uint32_t t = threadIdx.x, b0 = t * PER;
-    uint32_t local[PER];
-    uint32_t sum = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < PER; i++) {
-        local[i] = L.hist[b0 + i];
-        sum += local[i];
-    }
-    uint32_t incl = sum;
+    const uint32_t t = threadIdx.x;
+    T incl = v;
     for (int o = 1; o < 64; o <<= 1) {
-        uint32_t v = (uint32_t)__shfl_up((int)incl, o, 64);
-        if ((t & 63u) >= (uint32_t)o) incl += v;
+        T u = __shfl_up(incl, o, 64);
+        if ((t & 63u) >= (uint32_t)o) incl += u;
     }
     if ((t & 63u) == 63u) wsum[t >> 6] = incl;
     __syncthreads();
-    uint32_t before = 0;
-    for (uint32_t w = 0; w < (t >> 6); w++) before += wsum[w];
-    uint32_t run = before + incl - sum;
+    T before = 0, all = 0;
+    for (uint32_t w = 0; w < GS_THREADS / 64; w++) {
+        before += w < (t >> 6) ? wsum[w] : T(0);
+        all += wsum[w];
+    }
+    __syncthreads();   // wsum reusable
+    *total = all;
+    return before + incl - v;
+}
+
+// Longest-first bin order (dslots::gcost).  A bin's cost is the mean extend
+// time over the positions its rays held in the previous round (binprev): the
+// extend blocks' times (the sum of a block's four wave times, one uint4 of
+// tilecost) as prefix sums in LDS over units of U blocks (at most GS_PREFIX
+// units), linearly interpolated inside a unit, bucketed like tile_order_kernel (16
+// buckets per octave; bins the previous round did not see go last).  Only
+// the bins that hold rays this round are ranked (about a quarter on C3).
+// tools/exp_bincost.py: on C3's settled rays this order traces in 0.70-0.74x
+// of slot order against 0.78-0.79x for key order with block-index
+// longest-first (profiles/r03_bincost).
+constexpr uint32_t GS_PREFIX = 8192;   // LDS prefix entries (32 KB)
+
+// The sort pass's scan (one block of GS_THREADS): cursor[b] = first position
+// of bin b (bins in key order, or longest first with gcost), cursor[PT_GS_BINS]
+// = *nvalid = all valid rays (slots outside the image follow); binprev
+// records the ranges for the next round; the counts cleared.  Every global
+// load is issued at the start (one memory latency), the rest runs in LDS.
+PT_DEV void GsScan(const dslots& L, uint32_t* cursor)
+{
+    constexpr uint32_t PER = PT_GS_BINS / GS_THREADS;
+    constexpr uint32_t PE = GS_PREFIX / GS_THREADS;   // prefix entries per thread
+    __shared__ uint32_t wsum[GS_THREADS / 64];
+    __shared__ float fsum[GS_THREADS / 64];
+    __shared__ uint32_t bucket[512];
+    __shared__ uint32_t byrank[PT_GS_BINS];
+    __shared__ float pre[GS_PREFIX + 1];
+    const uint32_t t = threadIdx.x, b0 = t * PER;
+    uint32_t cnt[PER], rank[PER];
+    uint2 pv[PER];
 #pragma unroll
     for (uint32_t i = 0; i < PER; i++) {
-        cursor[b0 + i] = run;
-        run += local[i];
+        cnt[i] = L.hist[b0 + i];
+        rank[i] = b0 + i;
+    }
+    if (L.gcost) {
+        // Units of U blocks (U = 1 while the frame has <= GS_PREFIX blocks).
+        const uint32_t nb = L.n / 256, U = (nb + GS_PREFIX - 1) / GS_PREFIX;
+        const uint32_t ne = (nb + U - 1) / U;
+        const uint4* tc = reinterpret_cast<const uint4*>(L.tilecost);
+        float v[PE];
+#pragma unroll
+        for (uint32_t j = 0; j < PE; j++) v[j] = 0;
+        for (uint32_t u = 0; u < U; u++) {
+#pragma unroll
+            for (uint32_t j = 0; j < PE; j++) {
+                const uint32_t blk = (t * PE + j) * U + u;
+                uint4 c = blk < nb ? tc[blk] : make_uint4(0, 0, 0, 0);
+                v[j] += (float)(c.x + c.y + c.z + c.w);
+            }
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) pv[i] = L.binprev[b0 + i];
+        float sum = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < PE; j++) sum += v[j];
+        float all;
+        float run = GsBlockScan(sum, fsum, &all);
+#pragma unroll
+        for (uint32_t j = 0; j < PE; j++) {
+            pre[t * PE + j] = run;
+            run += v[j];
+        }
+        if (t == GS_THREADS - 1) pre[GS_PREFIX] = all;
+        for (uint32_t i = t; i < 512; i += GS_THREADS) bucket[i] = 0;
+        __syncthreads();
+        const float unit = 256.0f * (float)U;
+        auto at = [&](uint32_t p) -> float {
+            const uint32_t e = min(p / (256u * U), ne);
+            const float f = (float)(p - e * 256u * U) / unit;
+            const float a = pre[e];
+            return e < ne ? a + (pre[e + 1] - a) * f : a;
+        };
+        uint32_t key[PER];
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) {
+            key[i] = 511u;
+            if (cnt[i] && pv[i].y) {
+                // mean time per wave of 64 positions
+                float c = (at(pv[i].x + pv[i].y) - at(pv[i].x)) / (float)pv[i].y * 64.0f;
+                if (c >= 16.0f) {
+                    uint32_t ci = (uint32_t)fminf(c, 4.0e9f);
+                    uint32_t e = 31u - __clz(ci);
+                    uint32_t m = (ci >> (e - 4)) & 15u;
+                    key[i] = 511u - min(e * 16u + m, 511u);
+                }
+            }
+            if (cnt[i]) atomicAdd(&bucket[key[i]], 1u);
+        }
+        __syncthreads();
+        uint32_t c = t < 512 ? bucket[t] : 0u, tot;
+        uint32_t start = GsBlockScan(c, wsum, &tot);
+        if (t < 512) bucket[t] = start;
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) byrank[b0 + i] = 0;
+        __syncthreads();
+        // Rank inside a bucket by LDS atomic: any order of the bins gives the
+        // same results (only the dispatch order of the rays changes).  The
+        // empty bins take no rank (their cursor is never used).
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) rank[i] = cnt[i] ? atomicAdd(&bucket[key[i]], 1u) : 0u;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++)
+            if (cnt[i]) byrank[rank[i]] = cnt[i];
+    } else {
+#pragma unroll
+        for (uint32_t i = 0; i < PER; i++) byrank[rank[i]] = cnt[i];
+    }
+    // Counts by rank, their exclusive prefix sums, back to the bins.
+    __syncthreads();
+    uint32_t r[PER], sum = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < PER; i++) {
+        r[i] = byrank[b0 + i];
+        sum += r[i];
+    }
+    uint32_t total;
+    uint32_t run = GsBlockScan(sum, wsum, &total);
+#pragma unroll
+    for (uint32_t i = 0; i < PER; i++) {
+        byrank[b0 + i] = run;
+        run += r[i];
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t i = 0; i < PER; i++) {
+        uint32_t first = byrank[rank[i]];
+        cursor[b0 + i] = first;
+        L.binprev[b0 + i] = make_uint2(first, cnt[i]);
         L.hist[b0 + i] = 0;
     }
-    if (t == GS_THREADS - 1) { cursor[PT_GS_BINS] = run; *L.nvalid = run; }
+    if (t == GS_THREADS - 1) { cursor[PT_GS_BINS] = total; *L.nvalid = total; }
 }
 
 // Global ray sort pass (before each extend), three launches over the key
 // bins (PT_GS_BINS + one for slots outside the image):
 //   gsort_count_kernel    per chunk of GS_CHUNK slots an LDS histogram of the
 //                         keys, one global add per nonzero bin;
-//   gsort_scan_kernel     the bins' exclusive prefix sums (GsScan);
+//   gsort_scan_kernel     the bins' first positions (GsScan: key order, or
+//                         longest first by the previous round's cost);
 //   gsort_scatter_kernel  per chunk again: each nonzero bin reserves its range
 //                         with one global atomic, each slot takes the next
 //                         position of its bin's range (LDS atomic) and
-//                         records it (gpos) and itself there (perm).
+//                         records itself there (perm).
 // (Copying the rays into sorted order instead of extend gathering them
 // through perm: scatter +8 us, shade +10 us, extend -6 us; not kept.)
 // Same-address global atomics per ray serialise badly (camera rays share one
@@ -1284,7 +1421,6 @@ __global__ __launch_bounds__(GS_THREADS) void gsort_scatter_kernel(dslots L, dfr
         uint32_t s = s0 + i * GS_THREADS + threadIdx.x;
         if (s >= L.n) continue;
         uint32_t q = atomicAdd(&cnt[k[i]], 1u);
-        L.gpos[s] = q;
         if (k[i] < PT_GS_BINS) L.perm[q] = s;
     }
 }
@@ -1397,11 +1533,10 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
     const uint32_t base = tile * 256;
     uint32_t s, p16 = 0;
     if (L.gsort) {
-        // Global ray sort: the tile's outcome classes come from the positions
-        // its rays were traced at (one gathered byte per slot); the class
-        // masks are built in LDS, then ShadeOrder as below, by slot.
+        // Global ray sort: extend left each slot's outcome class by slot; the
+        // tile's class masks are built in LDS, then ShadeOrder as below.
         __shared__ uint64_t gm[4 * PT_OUTCOME_CLASSES];
-        uint32_t c = L.cls[L.gpos[base | threadIdx.x]];
+        uint32_t c = L.cls[base | threadIdx.x];
         uint32_t w = threadIdx.x >> 6;
 #pragma unroll
         for (uint32_t k = 0; k < PT_OUTCOME_CLASSES; k++) {
@@ -1453,8 +1588,8 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
         // (Trace, scene.glsl.inc:535-608) are rebuilt here and go through the
         // same octahedral snorm16 quantisation as the reference's
         // StoreTraceHit / LoadTraceResult.
-        uint32_t q = L.gsort ? L.gpos[s] : RayPos(L, s, p16);
-        float4 r = L.ray[L.gsort ? s : q];
+        uint32_t q = L.gsort ? s : RayPos(L, s, p16);
+        float4 r = L.ray[q];
         O = v3(r.x, r.y, r.z);
         V = UnpackUnitVector(__float_as_uint(r.w));
         float4 h = L.hit[q];

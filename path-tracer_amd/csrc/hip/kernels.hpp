@@ -43,12 +43,12 @@ struct dslots {
     // tile.  `ray` is then indexed by slot, and:
     uint32_t* perm;     // per position: the slot whose ray extend traces there
     uint32_t* nvalid;   // positions [0, *nvalid) hold rays (slots inside the image)
-    uint32_t* gpos;     // per slot: position of its ray in the last extend
     uint16_t* key;      // per slot: sort key of its current ray (RayKey, written by raygen / shade)
-    uint32_t* hist;     // per key bin: the frame's count (sort pass; cleared by the scan);
-                        // hist[PT_GS_BINS + 1]: the count kernel's block ticket
+    uint32_t* hist;     // per key bin: the frame's count (sort pass; cleared by the scan)
     uint8_t* cls;       // per position: the traced ray's ShadeOrder outcome class
+    uint2* binprev;     // per key bin: {first position, count} in the last extend
     uint32_t gsort;
+    uint32_t gcost;     // bins in descending order of their previous-round cost (else key order)
     uint32_t n;
     // The launch's tile range (a run group, runtime.hip): tiles
     // [tile_base, tile_base + tile_count); `order` then points at the group's
@@ -102,7 +102,7 @@ hipError_t pt_launch_resolve(const float4* accum, uint32_t n, float brightness, 
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
                            uint32_t scene_mats, hipStream_t st);
 // Global ray sort before an extend: key counts (hist), their exclusive prefix
-// sums (cursor, hist cleared), then every slot's position (gpos, perm).  PT_GS_BINS key bins + one for slots outside the image.
+// sums (cursor, hist cleared), then every position's slot (perm).  PT_GS_BINS key bins + one for slots outside the image.
 constexpr uint32_t PT_GS_BINS = 4096;
 hipError_t pt_launch_gsort(const ptd::dslots& L, const ptd::dframe& F, uint32_t* cursor, hipStream_t st);
 hipError_t pt_launch_vertex_decode(const uint2* v, uint32_t n, float4* attr, float* vv, hipStream_t st);

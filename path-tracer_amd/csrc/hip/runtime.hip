@@ -162,9 +162,10 @@ struct pt_basic_renderer {
     dbuf<uint32_t> done;                // per wave: completed paths since the last Reset (ptGetStats)
     // Global ray sort (PT_GLOBAL_SORT, kernels.hip): per-position slot, per-slot
     // position and key, key-bin counts and cursors, per-position outcome class.
-    dbuf<uint32_t> perm, nvalid, gpos, hist, cursor;
+    dbuf<uint32_t> perm, nvalid, hist, cursor;
     dbuf<uint16_t> key;
     dbuf<uint8_t> cls;
+    dbuf<uint2> binprev;
     // Run groups: the tiles split into `groups` contiguous ranges, each
     // advanced round by round on its own stream, so a group's next round
     // starts while another group's extend is still draining its longest
@@ -753,6 +754,14 @@ static bool GlobalSortEnabled()
     return e && atoi(e) != 0;
 }
 
+// PT_GS_COST=0: the global sort keeps its bins in key order instead of
+// longest first by the previous round's cost (GsScan).
+static bool GlobalSortCostOrder()
+{
+    const char* e = getenv("PT_GS_COST");
+    return !(e && atoi(e) == 0);
+}
+
 // PT_TILE_ORDER=0: extend dispatches tiles in their natural order.
 static bool TileOrderEnabled()
 {
@@ -827,9 +836,11 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     r->slots.done = r->done.ptr;
     r->slots.spill = nullptr;
     r->slots.gsort = 0;
-    r->slots.perm = nullptr; r->slots.nvalid = nullptr; r->slots.gpos = nullptr; r->slots.key = nullptr;
+    r->slots.perm = nullptr; r->slots.nvalid = nullptr; r->slots.key = nullptr;
     r->slots.hist = nullptr;
     r->slots.cls = nullptr;
+    r->slots.binprev = nullptr;
+    r->slots.gcost = 0;
     r->slots.n = ns;
     r->slots.tile_base = 0;
     r->slots.tile_count = ns / 256;
@@ -837,17 +848,22 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     if (GlobalSortEnabled() && ns && r->groups == 1) {
         const size_t nb = PT_GS_BINS + 1;
         ok = r->perm.alloc(ns) == hipSuccess && r->nvalid.alloc(1) == hipSuccess &&
-             r->gpos.alloc(ns) == hipSuccess &&
              r->key.alloc(ns) == hipSuccess && r->hist.alloc(nb) == hipSuccess && r->cursor.alloc(nb) == hipSuccess &&
-             r->cls.alloc(ns) == hipSuccess &&
+             r->cls.alloc(ns) == hipSuccess && r->binprev.alloc(PT_GS_BINS) == hipSuccess &&
+             hipMemset(r->binprev.ptr, 0, (size_t)PT_GS_BINS * 8) == hipSuccess &&
+             hipMemset(r->tilecost.ptr, 0, ((size_t)(ns / 256) * 4 + 1) * 4) == hipSuccess &&
              hipMemset(r->perm.ptr, 0, (size_t)ns * 4) == hipSuccess &&
              hipMemset(r->nvalid.ptr, 0, 4) == hipSuccess &&
-             hipMemset(r->gpos.ptr, 0, (size_t)ns * 4) == hipSuccess &&
              hipMemset(r->key.ptr, 0, (size_t)ns * 2) == hipSuccess && hipMemset(r->hist.ptr, 0, nb * 4) == hipSuccess &&
              hipMemset(r->cls.ptr, 0, ns) == hipSuccess;
         r->slots.gsort = 1;
-        r->slots.perm = r->perm.ptr; r->slots.nvalid = r->nvalid.ptr; r->slots.gpos = r->gpos.ptr; r->slots.key = r->key.ptr;
+        r->slots.perm = r->perm.ptr; r->slots.nvalid = r->nvalid.ptr; r->slots.key = r->key.ptr;
         r->slots.hist = r->hist.ptr; r->slots.cls = r->cls.ptr;
+        r->slots.binprev = r->binprev.ptr;
+        r->slots.gcost = GlobalSortCostOrder() ? 1u : 0u;
+        // Extend's dispatch order is then the sort's (longest-first bins);
+        // shade takes its tiles in natural order.
+        r->slots.order = nullptr;
         if (!ok) {
             SetError("renderer global-sort allocation failed (%u slots)", ns);
             ptDestroyBasicRenderer(d, r);
@@ -884,8 +900,8 @@ void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
     r->tilecost.release(); r->order.release();
     r->done.release();
     r->spill.release();
-    r->perm.release(); r->nvalid.release(); r->gpos.release(); r->key.release(); r->hist.release(); r->cursor.release();
-    r->cls.release();
+    r->perm.release(); r->nvalid.release(); r->key.release(); r->hist.release(); r->cursor.release();
+    r->cls.release(); r->binprev.release();
     for (uint32_t g = 0; g < pt_basic_renderer::MAX_GROUPS; g++) {
         if (r->gstream[g]) (void)hipStreamDestroy(r->gstream[g]);
         if (r->gevent[g]) (void)hipEventDestroy(r->gevent[g]);
@@ -1124,8 +1140,6 @@ int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state*
     PT_HIP(hipMemcpy(lam.data(), r->lam.ptr, (size_t)n * 4, hipMemcpyDeviceToHost));
     PT_HIP(hipMemcpy(act.data(), r->act.ptr, (size_t)n * 8, hipMemcpyDeviceToHost));
     PT_HIP(hipMemcpy(pos.data(), r->pos.ptr, (size_t)n * 2, hipMemcpyDeviceToHost));
-    std::vector<uint32_t> gpos(r->slots.gsort ? n : 0);
-    if (r->slots.gsort) PT_HIP(hipMemcpy(gpos.data(), r->gpos.ptr, (size_t)n * 4, hipMemcpyDeviceToHost));
     uint32_t W = r->buffer->width, H = r->buffer->height;
     auto bits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
     for (uint32_t s = 0; s < n; s++) {
@@ -1134,9 +1148,9 @@ int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state*
         if (x >= W || y >= H) continue;
         pt_pixel_state& O = out[(size_t)y * W + x];
         // Ray and hit records live at the slot's TileOrder positions (global
-        // sort: the ray by slot, the hit at the slot's last extend position).
+        // sort: both by slot).
         uint32_t qr = (s & ~255u) | (pos[s] >> 8u), qh = (s & ~255u) | (pos[s] & 255u);
-        if (r->slots.gsort) { qr = s; qh = gpos[s]; }
+        if (r->slots.gsort) { qr = s; qh = s; }
         O.origin[0] = ray[qr].x; O.origin[1] = ray[qr].y; O.origin[2] = ray[qr].z;
         O.packed_velocity = bits(ray[qr].w);
         O.hit.time = hit[qh].x;
