@@ -200,6 +200,19 @@ uint32_t           ptBasicRendererRunGroups(pt_basic_renderer* renderer);
  * scene allows (no spilled traversal stack).  Results are identical in every
  * mode.  Default 1, or the PT_ROUND_FUSED environment variable. */
 int                ptSetBasicRendererFusedRounds(pt_basic_renderer* renderer, int mode);
+/* Consecutive rounds: ptRunBasicRendererRounds(d, r, k) is k calls of
+ * ptRunBasicRenderer(d, r, 1) -- the application's frame loop, one new
+ * FrameIndex per round (application.cpp:100-115) -- with identical results.
+ * Round batches run up to R of those rounds in one launch, each tile
+ * advancing through them without a grid-wide barrier between rounds (a slot's
+ * round depends only on its own previous round).  ptSetBasicRendererRoundBatch:
+ * 0 = automatic (16 rounds per launch when every tile of the renderer fits on
+ * the GPU at once and fused rounds are automatic, else one round per launch
+ * pair), 1 = never, R >= 2 = R whenever the scene allows (no spilled stack).
+ * Default 0, or the PT_ROUND_BATCH environment variable.  ptRenderFrame runs
+ * its Run(1) rounds this way. */
+int                ptRunBasicRendererRounds(pt_device* device, pt_basic_renderer* renderer, uint32_t count);
+int                ptSetBasicRendererRoundBatch(pt_basic_renderer* renderer, uint32_t rounds);
 /* OpenPBR shading (opt-in extension, no reference counterpart): 0 (default)
  * = an OpenPBR hit ends its path with no contribution, as in the reference,
  * whose integrator does not compile its OpenPBR BSDF (scene.glsl.inc:685);

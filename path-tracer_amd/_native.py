@@ -235,6 +235,8 @@ HIP_API = {
     "ptBasicRendererSlotCount": (_u32, [_vp]),
     "ptBasicRendererRunGroups": (_u32, [_vp]),
     "ptSetBasicRendererFusedRounds": (_i32, [_vp, _i32]),
+    "ptRunBasicRendererRounds": (_i32, [_vp, _vp, _u32]),
+    "ptSetBasicRendererRoundBatch": (_i32, [_vp, _u32]),
     "ptSetBasicRendererOpenPBR": (_i32, [_vp, _i32]),
     "ptGetStats": (_i32, [_vp, _vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "ptTraceRaysStats": (_i32, [_vp, _vp, _u32, _fptr, _u32ptr, _fptr, C.POINTER(C.c_uint64), _vp]),

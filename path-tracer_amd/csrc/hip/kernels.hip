@@ -1665,6 +1665,38 @@ __global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void round_kernel(
     ShadeTile<MATS>(S, L, F, Pm, tile);
 }
 
+// Round batches: Pm.rounds rounds of one tile per block.  A slot's round
+// depends only on its own previous round (its ray, path record and pixel;
+// the seed is the round's FrameIndex), so tiles need no grid-wide barrier
+// between rounds: a block runs its tile's extend and shade Pm.rounds times
+// with the seeds of consecutive Run(1) calls (seed_step 1) or of one Run(R)
+// (seed_step 0), and the launch has one tail per batch instead of two per
+// round.  Barriers between the phases make the tile's hits (extend -> shade)
+// and new rays (shade -> next extend, TileOrder positions) visible to the
+// block's other waves.  The block's whole time is the tile's cost for the
+// next batch's longest-first order.
+#ifndef PT_ROUNDS_MINW
+#define PT_ROUNDS_MINW 0
+#endif
+template <uint32_t MATS, int CAP, class E>
+__global__ __launch_bounds__(256, PT_ROUNDS_MINW ? PT_ROUNDS_MINW : ShadeMinWaves<MATS>()) void rounds_kernel(
+    dscene S, dslots L, dframe F, dparams Pm)
+{
+    __shared__ E smem[CAP * 256];
+    const uint32_t tile = L.order ? L.order[blockIdx.x] : L.tile_base + blockIdx.x;
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    dparams P = Pm;
+    for (uint32_t i = 0; i < Pm.rounds; i++) {
+        ExtendTile<ray_source_slots, false, CAP, E>(S, ray_source_slots{L, F}, L.n, nullptr, 0, smem, tile, false);
+        __syncthreads();
+        ShadeTile<MATS>(S, L, F, P, tile);
+        __syncthreads();
+        P.seed += Pm.seed_step;
+    }
+    if (L.order && (threadIdx.x & 63u) == 0)
+        L.tilecost[tile * 4 + (threadIdx.x >> 6)] = (uint32_t)(__builtin_amdgcn_s_memtime() - t0);
+}
+
 // Exhaustive check of FastRcp: every bit pattern d = i (i < 2^32); counts
 // d in FastRcpRange whose FastRcp(d) differs from 1.0f / d in any bit.
 __global__ __launch_bounds__(256) void rcp_check_kernel(unsigned long long* mismatches)
@@ -1937,6 +1969,41 @@ hipError_t pt_launch_round(const ptd::dscene& S, const ptd::dslots& L, const ptd
     if (L.n == 0 || L.tile_count == 0) return hipSuccess;
     if (L.spill || pt_extend_variant() != 0) return hipErrorNotSupported;
     const void* k = RoundKernelFor(scene_mats, S.stack16 != 0);
+    void* args[] = {const_cast<ptd::dscene*>(&S), const_cast<ptd::dslots*>(&L), const_cast<ptd::dframe*>(&F),
+                    const_cast<ptd::dparams*>(&P)};
+    return hipLaunchKernel(k, dim3(L.tile_count), dim3(256), args, 0, st);
+}
+
+template <uint32_t MATS, class E>
+static const void* RoundsKernel() { return reinterpret_cast<const void*>(&ptd::rounds_kernel<MATS, 20, E>); }
+
+static const void* RoundsKernelFor(uint32_t mats, bool stack16)
+{
+    switch (pt_shade_mats(mats)) {
+    case PT_MATS_DIFFUSE: return stack16 ? RoundsKernel<PT_MATS_DIFFUSE, uint16_t>() : RoundsKernel<PT_MATS_DIFFUSE, uint32_t>();
+    case PT_MATS_DIFFUSE | PT_MATS_METAL:
+        return stack16 ? RoundsKernel<PT_MATS_DIFFUSE | PT_MATS_METAL, uint16_t>()
+                       : RoundsKernel<PT_MATS_DIFFUSE | PT_MATS_METAL, uint32_t>();
+    case PT_MATS_ALL: return stack16 ? RoundsKernel<PT_MATS_ALL, uint16_t>() : RoundsKernel<PT_MATS_ALL, uint32_t>();
+    default:
+        return stack16 ? RoundsKernel<PT_MATS_ALL | PT_MATS_OPENPBR, uint16_t>()
+                       : RoundsKernel<PT_MATS_ALL | PT_MATS_OPENPBR, uint32_t>();
+    }
+}
+
+// Round batches need the round kernel's conditions: no spilled stack, the
+// default extend variant, tile order (not the global sort).
+bool pt_rounds_available(const ptd::dslots& L)
+{
+    return !L.spill && !L.gsort && pt_extend_variant() == 0;
+}
+
+hipError_t pt_launch_rounds(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
+                            uint32_t scene_mats, hipStream_t st)
+{
+    if (L.n == 0 || L.tile_count == 0 || P.rounds == 0) return hipSuccess;
+    if (!pt_rounds_available(L)) return hipErrorNotSupported;
+    const void* k = RoundsKernelFor(scene_mats, S.stack16 != 0);
     void* args[] = {const_cast<ptd::dscene*>(&S), const_cast<ptd::dslots*>(&L), const_cast<ptd::dframe*>(&F),
                     const_cast<ptd::dparams*>(&P)};
     return hipLaunchKernel(k, dim3(L.tile_count), dim3(256), args, 0, st);

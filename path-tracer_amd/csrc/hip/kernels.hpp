@@ -70,6 +70,10 @@ struct dparams {
     uint32_t render_flags;
     float termination_probability;
     uint32_t seed;
+    // Round batches (rounds_kernel): rounds per launch, and the seed step
+    // between them (1: consecutive Run(1) calls, 0: one Run(R)).
+    uint32_t rounds = 1;
+    uint32_t seed_step = 0;
 };
 
 }  // namespace ptd
@@ -113,6 +117,11 @@ hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st);
 uint32_t pt_round_capacity(uint32_t scene_mats, bool stack16, uint32_t cu_count);
 hipError_t pt_launch_round(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
                            uint32_t scene_mats, hipStream_t st);
+// Round batch: P.rounds rounds (extend + shade) of every tile in one launch,
+// each block running its own tile through all of them (rounds_kernel).
+hipError_t pt_launch_rounds(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
+                            uint32_t scene_mats, hipStream_t st);
+bool pt_rounds_available(const ptd::dslots& L);
 // Zeroes the rows of a sample buffer outside a renderer's 16-row bands
 // (b % nranks != rank) before a frame-end reduce.
 hipError_t pt_launch_zero_unowned(float4* accum, uint32_t width, uint32_t height, uint32_t rank, uint32_t nranks,

@@ -140,6 +140,19 @@ int FusedDefault()
     const char* e = getenv("PT_ROUND_FUSED");
     return e ? atoi(e) : 1;
 }
+
+// Round-batch mode (ptSetBasicRendererRoundBatch): the PT_ROUND_BATCH
+// environment variable, else 0 (automatic).
+uint32_t RoundBatchDefault()
+{
+    const char* e = getenv("PT_ROUND_BATCH");
+    int x = e ? atoi(e) : 0;
+    return (uint32_t)std::max(0, x);
+}
+
+// Automatic mode's batch for a renderer whose tiles all fit on the GPU at
+// once (RoundFused's condition): one launch per AUTO_BATCH rounds.
+constexpr uint32_t AUTO_BATCH = 16;
 }  // namespace
 
 struct pt_basic_renderer {
@@ -174,6 +187,7 @@ struct pt_basic_renderer {
     uint32_t groups = 1;
     int fused = FusedDefault();         // fused rounds mode (ptSetBasicRendererFusedRounds)
     int openpbr = 0;                    // shade OpenPBR materials (ptSetBasicRendererOpenPBR)
+    uint32_t round_batch = RoundBatchDefault();   // rounds per launch of consecutive Run(1) rounds
     hipStream_t gstream[MAX_GROUPS] = {};
     hipEvent_t gevent[MAX_GROUPS] = {};
     hipEvent_t fork = nullptr;
@@ -1030,6 +1044,62 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
     return e ? e : j;
 }
 
+// k consecutive Run(1) calls: the same rounds with the same seeds (FrameIndex
+// + 1 ... + k), as round batches (rounds_kernel) when the renderer allows
+// them, else one ptRunBasicRenderer(1) per round.  round_batch: 0 automatic
+// (AUTO_BATCH rounds per launch when every tile fits on the GPU at once, where
+// the per-round launches cost most: C1 256x256 round 0.0176 -> 0.0055 ms;
+// whole frames that do not fit run slower batched -- C3 0.431 vs 0.47-0.53
+// ms per round, C2 -22 %: extend then runs at the shade kernel's occupancy and
+// the block's waves wait at the round's barriers), 1 never, R >= 2 always R.
+static int RunRounds(pt_device* d, pt_basic_renderer* r, uint64_t k)
+{
+    if (!r || CheckReady(r) != 0) return -1;
+    uint32_t B = r->round_batch;
+    if (B == 0) B = RoundFused(r, r->slots) && r->fused == 1 ? AUTO_BATCH : 1u;
+    if (B > 1 && r->groups == 1) {
+        PT_HIP(hipSetDevice(d->id));
+        if (int e = EnsureSpill(r)) return e;
+        if (pt_rounds_available(r->slots)) {
+            const ptd::dframe F = Frame(r);
+            while (k > 0) {
+                const uint32_t n = (uint32_t)std::min<uint64_t>(k, B);
+                ptd::dparams P = Params(r, r->params.FrameIndex + 1);
+                P.rounds = n;
+                P.seed_step = 1;
+                r->params.FrameIndex += n;
+                const bool sampled = d->profiling && (d->run_tick++ % d->profile_period) == 0;
+                event_pair ep{};
+                if (int e = BeginTimed(d, PT_KERNEL_ROUND, ep, sampled)) return e;
+                PT_HIP(pt_launch_rounds(r->scene->d, r->slots, F, P, ShadeMats(r), d->stream));
+                if (int e = EndTimed(d, ep)) return e;
+                // The batch's block times order the next batch.
+                if (r->slots.order) PT_HIP(pt_launch_tile_order(r->slots, d->stream));
+                r->rays += r->pixels * n;
+                k -= n;
+            }
+            return 0;
+        }
+    }
+    for (uint64_t i = 0; i < k; i++)
+        if (int e = ptRunBasicRenderer(d, r, 1)) return e;
+    return 0;
+}
+
+int ptRunBasicRendererRounds(pt_device* d, pt_basic_renderer* r, uint32_t count)
+{
+    if (!d) { SetError("null device"); return -1; }
+    if (CheckReady(r) != 0) return -1;
+    return RunRounds(d, r, count);
+}
+
+int ptSetBasicRendererRoundBatch(pt_basic_renderer* r, uint32_t rounds)
+{
+    if (!r) { SetError("ptSetBasicRendererRoundBatch: null renderer"); return -1; }
+    r->round_batch = rounds;
+    return 0;
+}
+
 uint32_t ptBasicRendererRunGroups(pt_basic_renderer* r) { return r ? r->groups : 0; }
 
 int ptSetBasicRendererFusedRounds(pt_basic_renderer* r, int mode)
@@ -1097,8 +1167,7 @@ int ptRenderFrame(pt_device* d, pt_basic_renderer* r, uint64_t target_samples, u
             k = std::max<uint64_t>(k, (uint64_t)(0.9 * (double)remaining / rate));
         }
         k = std::max<uint64_t>(1, std::min<uint64_t>(k, max_rounds - rounds));
-        for (uint64_t i = 0; i < k; i++)
-            if (int e = ptRunBasicRenderer(d, r, 1)) return e;
+        if (int e = RunRounds(d, r, k)) return e;
         rounds += (uint32_t)k;
         prev = samples;
         last_batch = (uint32_t)k;

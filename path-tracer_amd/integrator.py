@@ -244,6 +244,18 @@ class BasicRenderer:
         """0 never / 1 automatic / 2 whenever possible (ptSetBasicRendererFusedRounds)."""
         _check(N.hip_lib().ptSetBasicRendererFusedRounds(self._h, int(mode)), "ptSetBasicRendererFusedRounds")
 
+    def set_round_batch(self, rounds: int):
+        """Rounds per launch for consecutive Run(1) rounds (run_rounds,
+        render_frame): 0 automatic (16 when every tile fits on the GPU at
+        once), 1 never (one launch per round), R >= 2 always R."""
+        _check(N.hip_lib().ptSetBasicRendererRoundBatch(self._h, int(rounds)), "ptSetBasicRendererRoundBatch")
+
+    def run_rounds(self, count: int):
+        """count consecutive Run(1) calls (one new FrameIndex each), batched
+        per set_round_batch (ptRunBasicRendererRounds)."""
+        _check(N.hip_lib().ptRunBasicRendererRounds(self.device.handle, self._h, int(count)),
+               "ptRunBasicRendererRounds")
+
     def set_openpbr(self, enable: bool):
         """Shade OpenPBR materials (ptSetBasicRendererOpenPBR); off by default,
         as in the reference, where an OpenPBR hit ends the path."""

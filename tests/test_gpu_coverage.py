@@ -230,6 +230,73 @@ def test_fused_rounds_bit_exact(pt, dev, config, W, H, schedule):
     assert oa[..., 3].sum() > 0
 
 
+# (config, W, H, batch, count): count consecutive Run(1) rounds in batches of
+# `batch` per launch (a partial last batch when batch does not divide count),
+# small frames, C5's mixed materials and medium, and the full C3 frame.
+BATCH_CASES = [(3, 160, 96, 4, 7), (5, 128, 64, 3, 5), (2, 96, 96, 16, 9), (1, 64, 64, 2, 2),
+               (3, 1920, 1080, 4, 6), (5, 2048, 1024, 8, 8)]
+
+
+@pytest.mark.parametrize("config,W,H,batch,count", BATCH_CASES)
+def test_round_batches_bit_exact(pt, dev, config, W, H, batch, count):
+    """ptRunBasicRendererRounds with round batches (rounds_kernel: each tile
+    runs several rounds in one launch, seeds FrameIndex+1..+count) equals
+    `count` Run(1) calls on the oracle, state and image bit for bit; a Run(1)
+    through the per-round kernels follows the batches."""
+    from test_gpu_parity import scene_for
+    s = scene_for(pt, config)
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    sb = pt.SampleBuffer(dev, W, H)
+    r = pt.BasicRenderer(dev, ds, sb)
+    r.set_fused_rounds(0)
+    r.set_round_batch(batch)
+    o = oracle_lib.OracleRenderer(s.packs(), W, H)
+    for x in (r, o):
+        x.RenderFlags = 3
+        x.reset()
+        x.run(2)
+    r.run_rounds(count)
+    for _ in range(count):
+        o.run(1)
+    dev.synchronize()
+    compare_state(r.read_state(), o.state())
+    assert np.array_equal(bits(sb.read()), bits(o.accum())), "after the batches"
+    r.run(1)
+    o.run(1)
+    dev.synchronize()
+    compare_state(r.read_state(), o.state())
+    ga, oa = sb.read(), o.accum()
+    assert np.array_equal(bits(ga), bits(oa)), "after a per-round Run(1)"
+    assert oa[..., 3].sum() > 0
+    for x in (r, sb, ds):
+        x.close()
+
+
+def test_render_frame_round_batches_equal_per_round(pt, dev):
+    """ptRenderFrame with round batches (16, and automatic: this frame's 240
+    tiles fit on the GPU at once) ends at the same round with the same
+    accumulator as with per-round launches (C3 scene, 320x192, 48 spp)."""
+    from test_gpu_parity import scene_for
+    s = scene_for(pt, 3)
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    out = {}
+    for batch in (1, 0, 16):
+        sb = pt.SampleBuffer(dev, 320, 192)
+        r = pt.BasicRenderer(dev, ds, sb)
+        r.set_round_batch(batch)
+        r.RenderFlags = 3
+        rounds, samples = r.render_frame(48 * 320 * 192)
+        out[batch] = (rounds, samples, sb.read())
+        for x in (r, sb):
+            x.close()
+    ds.close()
+    for batch in (0, 16):
+        assert out[1][:2] == out[batch][:2]
+        assert np.array_equal(bits(out[1][2]), bits(out[batch][2])), f"batch {batch}"
+
+
 def test_fused_rounds_mode_argument(pt, dev):
     s = pt.Scene.config(1)
     ds = pt.DeviceScene(dev)

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--configs", default="3,4")
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--groups", default="", help="comma list of PT_RUN_GROUPS values to try (default: the runtime's choice)")
+    ap.add_argument("--batches", default="0", help="comma list of round batches (ptSetBasicRendererRoundBatch) to try")
     args = ap.parse_args()
     pt = load_package()
     dev = pt.Device(0)
@@ -49,7 +50,9 @@ def main():
         W, H = scene.info.width, scene.info.height
         ds = pt.DeviceScene(dev)
         ds.update(scene)
-        for n, groups in [(int(x), g) for x in args.ns.split(",") for g in (args.groups.split(",") if args.groups else [None])]:
+        for n, groups, batch in [(int(x), g, int(b)) for x in args.ns.split(",")
+                                 for g in (args.groups.split(",") if args.groups else [None])
+                                 for b in args.batches.split(",")]:
             if groups is None:
                 os.environ.pop("PT_RUN_GROUPS", None)
             else:
@@ -57,6 +60,7 @@ def main():
             sb = pt.SampleBuffer(dev, W, H)
             r = pt.BasicRenderer(dev, ds, sb, rank=0, nranks=n)
             r.RenderFlags = scene.info.render_flags
+            r.set_round_batch(batch)
             r.reset()
             r.run(2)
             r.run(32)
@@ -65,20 +69,25 @@ def main():
             dev.reset_kernel_stats()
             rays0, _ = r.stats()
             t0 = time.perf_counter()
-            for _ in range(args.steps):
-                r.run(1)
+            if batch > 1:
+                r.run_rounds(args.steps)
+            else:
+                for _ in range(args.steps):
+                    r.run(1)
             dev.synchronize()
             dt = time.perf_counter() - t0
             rays1, _ = r.stats()
             ne, me = dev.kernel_stats(1)
             ns_, ms = dev.kernel_stats(2)
             nr, mr = dev.kernel_stats(5)
+            if batch > 1:
+                nr = args.steps   # round batches: per-round time
             dev.set_profiling(False)
             owned = int(np.sum(pt.owned_pixels(W, H, 0, n)))
             step_ms = dt / args.steps * 1e3
             row = {
                 "config": cfg, "frame": f"{W}x{H}", "n_gpus": n, "rank0_pixels": owned,
-                "rank0_tiles": r.slot_count // 256, "run_groups": r.run_groups,
+                "rank0_tiles": r.slot_count // 256, "run_groups": r.run_groups, "round_batch": batch,
                 "rank0_ms_per_step": round(step_ms, 4),
                 "rank0_mrays_per_s": round((rays1 - rays0) / dt / 1e6, 1),
                 "extend_ms": round(me / max(ne, 1), 4), "shade_ms": round(ms / max(ns_, 1), 4),
