@@ -69,7 +69,7 @@ def main():
             dev.reset_kernel_stats()
             rays0, _ = r.stats()
             t0 = time.perf_counter()
-            if batch > 1:
+            if batch != 1:                 # 0 = automatic round batches, R >= 2 = R per launch
                 r.run_rounds(args.steps)
             else:
                 for _ in range(args.steps):
@@ -80,8 +80,6 @@ def main():
             ne, me = dev.kernel_stats(1)
             ns_, ms = dev.kernel_stats(2)
             nr, mr = dev.kernel_stats(5)
-            if batch > 1:
-                nr = args.steps   # round batches: per-round time
             dev.set_profiling(False)
             owned = int(np.sum(pt.owned_pixels(W, H, 0, n)))
             step_ms = dt / args.steps * 1e3
@@ -91,7 +89,7 @@ def main():
                 "rank0_ms_per_step": round(step_ms, 4),
                 "rank0_mrays_per_s": round((rays1 - rays0) / dt / 1e6, 1),
                 "extend_ms": round(me / max(ne, 1), 4), "shade_ms": round(ms / max(ns_, 1), 4),
-                "round_ms": round(mr / max(nr, 1), 4),
+                "round_launch_ms": round(mr / max(nr, 1), 4),   # fused round / round batch launch
                 "predicted_frame_mrays_per_s": round(W * H / (step_ms * 1e-3) / 1e6, 1),
             }
             rows.append(row)
