@@ -293,8 +293,16 @@ def main():
     # target needs at one completed path per slot and round is broken: stop.
     max_rounds = 64 * spp + 64
 
+    last_note = [time.perf_counter()]
+
     def frame(record):
         rounds, samples = r.render_frame(target, max_rounds)
+        # A progress note on stderr at most every 20 s (long configs such as
+        # C5's 8192-spp frames), so a watcher sees the run is alive.
+        now = time.perf_counter()
+        if rank == 0 and now - last_note[0] > 20.0:
+            print(f"bench: frame done ({rounds} rounds, {samples} samples)", file=sys.stderr, flush=True)
+            last_note[0] = now
         if samples < target:
             raise RuntimeError(f"frame stopped at {rounds} rounds with {samples} of {target} samples")
         frame_end_exchange()

@@ -49,3 +49,33 @@ def test_random_scene_bit_exact(pt, dev, seed):
     compare_hits(ds.trace_rays(o, v, d), oracle_lib.trace_rays(s.packs(), o, v, d))
     ds.close()
     s.close()
+
+
+@pytest.mark.parametrize("seed", SEEDS[::3])
+def test_random_scene_round_batches_bit_exact(pt, dev, seed):
+    """Round batches (rounds_kernel: several Run(1) rounds of a tile in one
+    launch) on the random scenes: Reset, Run(2), then 5 rounds in batches of
+    3 (a partial last batch) against 5 oracle Run(1) calls."""
+    s, st = fuzz_scenes.build(pt, seed)
+    W, H = 72, 40
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    sb = pt.SampleBuffer(dev, W, H)
+    r = pt.BasicRenderer(dev, ds, sb)
+    r.set_round_batch(3)
+    o = oracle_lib.OracleRenderer(s.packs(), W, H)
+    for x in (r, o):
+        x.RenderFlags = st["flags"]
+        x.PathTerminationProbability = st["termination"]
+        x.reset()
+        x.run(2)
+    r.run_rounds(5)
+    for _ in range(5):
+        o.run(1)
+    dev.synchronize()
+    compare_state(r.read_state(), o.state())
+    assert np.array_equal(sb.read().view(np.uint32), o.accum().view(np.uint32))
+    o.close()
+    for x in (r, sb, ds):
+        x.close()
+    s.close()
