@@ -598,3 +598,44 @@ def test_editor_updates_bit_exact(pt, dev):
     for x in (r, sb, ds):
         x.close()
     s.close()
+
+
+def test_whole_1024spp_frame_bit_exact(pt, dev):
+    """A complete benchmark-mode frame (ptRenderFrame: Reset, Run(2), Run(1)
+    until the accumulator holds 1024 samples per pixel) of the
+    C3 scene at 480x270 (510 tiles: every tile resident at once, so the
+    automatic round batches run it; a ragged bottom band), with and without
+    round batches, against the oracle running the same schedule for the same
+    number of rounds: every accumulated pixel bit-identical."""
+    from test_gpu_parity import scene_for
+    s = scene_for(pt, 3)
+    W, H = 480, 270
+    target = 1024 * W * H
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    out = {}
+    for batch in (0, 1):
+        sb = pt.SampleBuffer(dev, W, H)
+        r = pt.BasicRenderer(dev, ds, sb)
+        r.set_round_batch(batch)
+        r.RenderFlags = 3
+        out[batch] = r.render_frame(target) + (sb.read(),)
+        for x in (r, sb):
+            x.close()
+    ds.close()
+    rounds, samples, ga = out[0]
+    assert out[1][:2] == (rounds, samples)
+    assert samples >= target and rounds > 1000
+    o = oracle_lib.OracleRenderer(s.packs(), W, H)
+    o.RenderFlags = 3
+    o.reset()
+    o.run(2)
+    for _ in range(rounds - 2):
+        o.run(1)
+    _, osamples = o.counters()
+    oa = o.accum()
+    o.close()
+    assert osamples == samples
+    assert int(oa[..., 3].astype(np.float64).sum()) == samples
+    for batch in (0, 1):
+        assert np.array_equal(bits(out[batch][2]), bits(oa)), f"round batch mode {batch}"
