@@ -1,6 +1,7 @@
 """Cross-check of the oracle's Trace() against a second restatement written
-independently from the GLSL (tests/trace_restatement.py): closest-hit time
-(bit for bit) and the packed shape / material index on random rays
+independently from the GLSL (tests/trace_restatement.py): the whole trace
+record bit for bit -- closest-hit time, packed shape / material index,
+octahedral normal and tangent, texture U, V (not for spheres) -- on random rays
 (axis-aligned and tiny-component cases included, tests/rays.py) and on real
 path rays -- the rays in flight after a few oracle rounds, which start on
 surfaces and graze edges -- for configs 1, 2, 3, 5 and random fuzz scenes.
@@ -34,12 +35,19 @@ def path_rays(scene, W, H, n, seed):
 def check(arrays, packs, origins, vel, dur):
     rec = oracle_lib.trace_rays(packs, origins, vel, dur)
     V = kat.unpack_unit_vector(vel)
-    times, sm = tr.trace_records(arrays, origins, V, dur)
+    times, sm, pn, ptg, uv = tr.trace_records(arrays, origins, V, dur)
     assert np.array_equal(sm, rec["shape_material"]), \
         f"shape/material differs at {np.flatnonzero(sm != rec['shape_material'])[:8].tolist()}"
     hit = sm != 0xFFFFFFFF
     assert np.array_equal(times[hit].view(np.uint32), rec["time"][hit].view(np.uint32)), \
         f"hit time differs at {np.flatnonzero(hit & (times.view(np.uint32) != rec['time'].view(np.uint32)))[:8].tolist()}"
+    for name, mine in (("packed_normal", pn), ("packed_tangent", ptg)):
+        bad = np.flatnonzero(hit & (mine != rec[name]))
+        assert bad.size == 0, f"{name} differs at {bad[:8].tolist()}"
+    has_uv = hit & ~np.isnan(uv[:, 0])
+    for k, name in enumerate(("u", "v")):
+        bad = np.flatnonzero(has_uv & (uv[:, k].view(np.uint32) != rec[name].view(np.uint32)))
+        assert bad.size == 0, f"{name} differs at {bad[:8].tolist()}"
     return int(hit.sum())
 
 

@@ -10,6 +10,9 @@ Follows, statement by statement:
   IntersectMeshFace     src/scene/scene.glsl.inc:304-334
   IntersectBoundingBox  src/core/common.glsl.inc:153-185
   InverseTransformRay   src/core/common.glsl.inc:84-91 (InverseTransformPosition/Vector :70-80)
+  hit attributes        src/scene/scene.glsl.inc:535-608 (SafeNormalize :93-100,
+                        TransformNormal / TransformDirection, ComputeTangentVector :113-117;
+                        octahedral packing from tests/kat.py)
 and the record packing of StoreTraceHit (src/integrator/basic.glsl.inc:142-156):
 ShapeAndMaterialIndex = Shape << 16 | Material, 0xFFFFFFFF on a miss.
 
@@ -23,6 +26,8 @@ for a few hundred rays per scene.
 from __future__ import annotations
 
 import numpy as np
+
+import kat
 
 f32 = np.float32
 INFINITY = f32(1e30)             # common.glsl.inc:4
@@ -81,12 +86,14 @@ def intersect_bounding_box(O, V, reach, mn, mx):
 
 
 class Hit:
-    __slots__ = ("time", "shape", "prim")
+    __slots__ = ("time", "shape", "prim", "kind", "coords")
 
     def __init__(self, duration):
         self.time = f32(duration)
         self.shape = SHAPE_INDEX_NONE
         self.prim = 0
+        self.kind = -1
+        self.coords = None
 
 
 class Scene:
@@ -98,6 +105,10 @@ class Scene:
         self.shape_material = [int(m) for m in sh["MaterialIndex"]]
         self.shape_root = [int(r) for r in sh["MeshRootNodeIndex"]]
         self.shape_from = [np.asarray(t, np.float32).reshape(16) for t in sh["Transform"]["From"]]
+        self.shape_to = [np.asarray(t, np.float32).reshape(16) for t in sh["Transform"]["To"]]
+        mv = arrays["mesh_vertices"]
+        self.vertex_normal = mv["PackedNormal"].astype(np.uint32)
+        self.vertex_uv = mv["PackedUV"].astype(np.uint32)
         sn = arrays["shape_nodes"]
         self.sn_min = [_v(x) for x in sn["Minimum"]]
         self.sn_max = [_v(x) for x in sn["Maximum"]]
@@ -112,6 +123,7 @@ class Scene:
         self.f0 = [_v(x) for x in mf["Position0"]]
         self.f1 = [_v(x) for x in mf["Position1"]]
         self.f2 = [_v(x) for x in mf["Position2"]]
+        self.fv = [(int(a), int(b), int(c)) for a, b, c in zip(mf["VertexIndex0"], mf["VertexIndex1"], mf["VertexIndex2"])]
         self.shape_count = int(arrays["globals"]["ShapeCount"][0])
 
 
@@ -140,6 +152,8 @@ def intersect_mesh_face(S, O, V, face, hit):
     hit.time = t
     hit.shape = MESH_FACE_OF_INSTANCE
     hit.prim = face
+    hit.kind = MESH
+    hit.coords = [(f32(1.0) - u) - v, u, v]
 
 
 def intersect_mesh_node(S, O, V, root, hit):
@@ -188,6 +202,7 @@ def intersect_shape(S, O, V, idx, hit):
             if t < 0 or t > hit.time:
                 return
             hit.time, hit.shape, hit.prim = t, idx, 0
+            hit.kind, hit.coords = PLANE, [O[i] + V[i] * t for i in range(3)]
         elif kind == SPHERE:
             vv = _dot(V, V)
             p = _dot(O, V)
@@ -204,6 +219,7 @@ def intersect_shape(S, O, V, idx, hit):
             if s < 0 or s > vv * hit.time:
                 return
             hit.time, hit.shape, hit.prim = s / vv, idx, 0
+            hit.kind, hit.coords = SPHERE, [O[i] + V[i] * hit.time for i in range(3)]
         elif kind == CUBE:
             lo = [(f32(-1.0) - O[i]) / V[i] for i in range(3)]
             hi = [(f32(1.0) - O[i]) / V[i] for i in range(3)]
@@ -217,6 +233,7 @@ def intersect_shape(S, O, V, idx, hit):
             if t >= hit.time:
                 return
             hit.time, hit.shape, hit.prim = t, idx, 0
+            hit.kind, hit.coords = CUBE, [O[i] + V[i] * t for i in range(3)]
 
 
 def trace(S, O, V, duration):
@@ -253,17 +270,111 @@ def trace(S, O, V, duration):
     return hit
 
 
+# --- hit attributes (scene.glsl.inc:535-608) -------------------------------------
+
+def _normalize(v):
+    """GLSL normalize under the convention: v * (1 / sqrt(dot(v, v)))."""
+    r = f32(1.0) / np.sqrt(_dot(v, v))
+    return [v[0] * r, v[1] * r, v[2] * r]
+
+
+def _safe_normalize(v):
+    """common.glsl.inc:93-100: V / sqrt(LenSq), or +Z for a tiny vector."""
+    lsq = _dot(v, v)
+    if lsq < f32(1e-12):
+        return [f32(0.0), f32(0.0), f32(1.0)]
+    d = np.sqrt(lsq)
+    return [v[0] / d, v[1] / d, v[2] / d]
+
+
+def _transform_normal(n, frm):
+    """common.glsl.inc TransformNormal: normalize((vec4(N, 0) * From).xyz)."""
+    z = f32(0.0)
+    return _normalize([((n[0] * frm[4 * c] + n[1] * frm[4 * c + 1]) + n[2] * frm[4 * c + 2]) + z * frm[4 * c + 3]
+                       for c in range(3)])
+
+
+def _transform_direction(d, to):
+    """normalize(TransformVector(D)) = normalize((To * vec4(D, 0)).xyz)."""
+    return _normalize(_mat_vec(to, d, 0.0))
+
+
+def _tangent(n):
+    """ComputeTangentVector (common.glsl.inc:113-117)."""
+    v = [f32(1.0), f32(0.0), f32(0.0)] if abs(n[0]) < f32(0.9) else [f32(0.0), f32(1.0), f32(0.0)]
+    return _normalize(_cross(v, n))
+
+
+def _half2(u):
+    lo = np.array([u & 0xFFFF], np.uint16).view(np.float16)[0]
+    hi = np.array([u >> 16], np.uint16).view(np.float16)[0]
+    return f32(lo), f32(hi)
+
+
+def _sign(x):
+    return f32(1.0) if x > 0 else (f32(-1.0) if x < 0 else f32(0.0))
+
+
+def hit_attributes(S, h):
+    """(Normal, TangentX, UV or None) of a hit; UV is None for spheres (their
+    atan2 is a convention function of the numerics layer, not restated)."""
+    to, frm = S.shape_to[h.shape], S.shape_from[h.shape]
+    c = h.coords
+    if h.kind == MESH:
+        i0, i1, i2 = S.fv[h.prim]
+        n0, n1, n2 = kat.unpack_unit_vector(np.array([S.vertex_normal[i0], S.vertex_normal[i1],
+                                                      S.vertex_normal[i2]], np.uint32))
+        n = [(n0[k] * c[0] + n1[k] * c[1]) + n2[k] * c[2] for k in range(3)]
+        normal = _transform_normal(_safe_normalize(n), frm)
+        tangent = _tangent(normal)
+        uv0, uv1, uv2 = _half2(int(S.vertex_uv[i0])), _half2(int(S.vertex_uv[i1])), _half2(int(S.vertex_uv[i2]))
+        uv = [(uv0[k] * c[0] + uv1[k] * c[1]) + uv2[k] * c[2] for k in range(2)]
+    elif h.kind == PLANE:
+        normal = _transform_normal([f32(0.0), f32(0.0), f32(1.0)], frm)
+        tangent = _transform_direction([f32(1.0), f32(0.0), f32(0.0)], to)
+        uv = [c[0] - np.floor(c[0]), c[1] - np.floor(c[1])]
+    elif h.kind == SPHERE:
+        normal = _transform_normal(c, frm)
+        tangent = _transform_direction(_cross(c, [-c[1], c[0], f32(0.0)]), to)
+        uv = None
+    else:
+        q = [abs(c[0]), abs(c[1]), abs(c[2])]
+        half, one = f32(0.5), f32(1.0)
+        if q[0] >= q[1] and q[0] >= q[2]:
+            sg = _sign(c[0])
+            nrm, tx, uv = [sg, f32(0), f32(0)], [f32(0), sg, f32(0)], [half * (one + c[1]), half * (one + c[2])]
+        elif q[1] >= q[0] and q[1] >= q[2]:
+            sg = _sign(c[1])
+            nrm, tx, uv = [f32(0), sg, f32(0)], [f32(0), f32(0), sg], [half * (one + c[0]), half * (one + c[2])]
+        else:
+            sg = _sign(c[2])
+            nrm, tx, uv = [f32(0), f32(0), sg], [sg, f32(0), f32(0)], [half * (one + c[0]), half * (one + c[1])]
+        normal = _transform_normal(nrm, frm)
+        tangent = _transform_direction(tx, to)
+    return normal, tangent, uv
+
+
 def trace_records(arrays, origins, velocities, durations):
-    """(time, ShapeAndMaterialIndex) per ray, as StoreTraceHit writes them."""
+    """Per ray, as StoreTraceHit (basic.glsl.inc:142-156) writes them: time,
+    ShapeAndMaterialIndex, packed normal, packed tangent, U, V (U, V NaN where
+    not restated: sphere hits)."""
     S = Scene(arrays)
     n = len(origins)
     times = np.zeros(n, np.float32)
     sm = np.zeros(n, np.uint32)
+    pn = np.zeros(n, np.uint32)
+    ptg = np.zeros(n, np.uint32)
+    uv = np.full((n, 2), np.nan, np.float32)
     for i in range(n):
         h = trace(S, origins[i], velocities[i], durations[i])
         if h.shape == SHAPE_INDEX_NONE:
             sm[i] = 0xFFFFFFFF
-        else:
-            sm[i] = (h.shape << 16) | S.shape_material[h.shape]
-            times[i] = h.time
-    return times, sm
+            continue
+        sm[i] = (h.shape << 16) | S.shape_material[h.shape]
+        times[i] = h.time
+        normal, tangent, u = hit_attributes(S, h)
+        pn[i] = kat.pack_unit_vector(np.array([normal], np.float32))[0]
+        ptg[i] = kat.pack_unit_vector(np.array([tangent], np.float32))[0]
+        if u is not None:
+            uv[i] = u
+    return times, sm, pn, ptg, uv
