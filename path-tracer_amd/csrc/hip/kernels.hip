@@ -491,13 +491,25 @@ PT_DEV bool SampleSurfaceIntegrand(const dscene& S, rng& G, pt3 Nrm, pt3 TX, pt3
     pt3 SMD = v3(S.g.SkyboxMeanDirection[0], S.g.SkyboxMeanDirection[1], S.g.SkyboxMeanDirection[2]);
     pt3 Mu = v3(dot(SMD, TX), dot(SMD, TY), dot(SMD, Nrm));
     bool ok;
-    if (G.R01() < LightProbability) {
+    const bool light = G.R01() < LightProbability;
+    const bool diffuse = (MATS & PT_MATS_DIFFUSE) && Type == PT_MATERIAL_TYPE_BASIC_DIFFUSE;
+    // A diffuse hit draws In by the light choice -- the sky lobe or the
+    // material's cosine sample -- and then evaluates the material with the
+    // same arguments either way (MaterialEvaluateBSDF / MaterialSampleBSDF of
+    // basic_diffuse.glsl.inc), so the evaluation (texture + spectrum) runs
+    // once after the join instead of in both divergent halves.
+    if (light) {
         In = RandomVonMisesFisher(G, vmf_consts{S.vmf_inv_kappa, S.vmf_exp_m2k, S.vmf_norm}, Mu);
         if (In.z < 0.0f) return false;
+    } else if (diffuse) {
+        In = SafeNormalize(RandomDirection(G) + v3(0, 0, 1));
+    }
+    if (diffuse) {
+        ok = Diffuse_Evaluate(S, P, Out, Throughput, MaterialPDF);
+        if (!ok) return false;
+    } else if (light) {
         // MaterialEvaluateBSDF(Parameters, Out, In, ...)
-        if ((MATS & PT_MATS_DIFFUSE) && Type == PT_MATERIAL_TYPE_BASIC_DIFFUSE)
-            ok = Diffuse_Evaluate(S, P, Out, Throughput, MaterialPDF);
-        else if ((MATS & PT_MATS_METAL) && Type == PT_MATERIAL_TYPE_BASIC_METAL)
+        if ((MATS & PT_MATS_METAL) && Type == PT_MATERIAL_TYPE_BASIC_METAL)
             ok = Metal_Evaluate(S, P, Out, In, Throughput, MaterialPDF);
         else if ((MATS & PT_MATS_TRANSLUCENT) && Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT)
             ok = Translucent_Evaluate(S, P, Out, In, Throughput, MaterialPDF);
@@ -505,10 +517,7 @@ PT_DEV bool SampleSurfaceIntegrand(const dscene& S, rng& G, pt3 Nrm, pt3 TX, pt3
         if (!ok) return false;
     } else {
         // MaterialSampleBSDF(Parameters, Out, In, ...)
-        if ((MATS & PT_MATS_DIFFUSE) && Type == PT_MATERIAL_TYPE_BASIC_DIFFUSE) {
-            In = SafeNormalize(RandomDirection(G) + v3(0, 0, 1));
-            ok = Diffuse_Evaluate(S, P, Out, Throughput, MaterialPDF);
-        } else if ((MATS & PT_MATS_METAL) && Type == PT_MATERIAL_TYPE_BASIC_METAL) {
+        if ((MATS & PT_MATS_METAL) && Type == PT_MATERIAL_TYPE_BASIC_METAL) {
             ok = Metal_Sample(S, G, P, Out, In, Throughput, MaterialPDF);
         } else if ((MATS & PT_MATS_TRANSLUCENT) && Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT) {
             ok = Translucent_Sample(S, G, P, Out, In, Throughput, MaterialPDF);
