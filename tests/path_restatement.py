@@ -1,0 +1,361 @@
+"""A second restatement of the integrator's rounds for BasicDiffuse scenes,
+written from the GLSL text apart from oracle/pt_oracle.cpp (test
+infrastructure only; tests/test_path_restatement.py).  With
+tests/trace_restatement.py for Trace() it re-derives, per pixel, what
+Reset / Run(k) leave in the slot state and the accumulator:
+
+  main (seeding, escape -> accumulate -> GenerateNewPath)  basic_scatter.glsl:312-360
+  GenerateNewPath / GenerateCameraRay                      basic_scatter.glsl:7-42, scene.glsl.inc:613-655
+  LoadTraceResult / LoadPath / StorePathVertexData         basic.glsl.inc:99-131,159-215
+  Scatter                                                  basic_scatter.glsl:114-310
+  ResolveMedium                                            basic_scatter.glsl:45-66
+  SampleSurfaceIntegrand                                   basic_scatter.glsl:68-109
+  BasicDiffuse_SampleBSDF / _EvaluateBSDF                  basic_diffuse.glsl.inc
+  MaterialTexturableReflectance, SampleTexture (nearest)   scene.glsl.inc:180-290
+  SampleSkyboxSpectrum / Radiance (no sky texture)         scene.glsl.inc:206-227
+  SampleParametricSpectrum, SampleStandardObserver         spectrum.glsl.inc:10-34,169-192
+  RandomDirection, RandomPointOnDisk, VonMisesFisherPDF    common.glsl.inc:205-254
+
+Scope: every material BasicDiffuse, textures nearest-filtered, no sky
+texture, SkyboxSamplingProbability 0 (C1's scene).
+Numerics: DESIGN.md §2's convention (float32, nothing fused, reductions left
+to right, normalize = v * (1 / sqrt(dot)), mix = x*(1-a) + y*a); exp, log,
+sin, cos are the convention's own functions (the oracle's exported pt_exp /
+pt_log / pt_sin / pt_cos), the octahedral packing tests/kat.py's.
+Nearest sampling follows the Vulkan rule i = floor(u * width), REPEAT.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+import kat
+import oracle_lib
+import trace_restatement as tr
+
+f32 = np.float32
+PI = f32(3.141592653)
+TAU = f32(6.283185306)
+EPSILON = f32(1e-9)
+HIT_TIME_LIMIT = f32(1048576.0)
+LAMBDA_MIN, LAMBDA_MAX = f32(360.0), f32(830.0)
+NONE = 0xFFFFFFFF
+
+
+def _fp(name, *a):
+    return f32(getattr(oracle_lib.lib(), f"oracle_fp_{name}")(*[float(x) for x in a]))
+
+
+class Rng:
+    """Random() / Random0To1() (common.glsl.inc:189-202) from main's seed."""
+
+    def __init__(self, x, y, frame):
+        self.state = kat.seed(x, y, frame)
+
+    def r01(self):
+        v, self.state = kat.pcg(self.state)
+        return f32(v) / f32(4294967296.0)
+
+
+def _mix(a, b, t):
+    return a * (f32(1.0) - t) + b * t
+
+
+def _fract(x):
+    return x - np.floor(x)
+
+
+def _normalize(v):
+    r = f32(1.0) / np.sqrt((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2])
+    return [v[0] * r, v[1] * r, v[2] * r]
+
+
+def _safe_normalize(v):
+    lsq = (v[0] * v[0] + v[1] * v[1]) + v[2] * v[2]
+    if lsq < f32(1e-12):
+        return [f32(0.0), f32(0.0), f32(1.0)]
+    d = np.sqrt(lsq)
+    return [v[0] / d, v[1] / d, v[2] / d]
+
+
+def _dot(a, b):
+    return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]
+
+
+def _cross(a, b):
+    return [a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]]
+
+
+def _mat_vec(m, v, w):
+    w = f32(w)
+    return [((m[r] * v[0] + m[4 + r] * v[1]) + m[8 + r] * v[2]) + m[12 + r] * w for r in range(3)]
+
+
+def _max4(v):
+    return np.fmax(np.fmax(v[0], v[1]), np.fmax(v[2], v[3]))
+
+
+def random_point_on_disk(g):
+    r = np.sqrt(g.r01())
+    theta = g.r01() * TAU
+    return r * _fp("cos", theta), r * _fp("sin", theta)
+
+
+def random_direction(g):
+    z = f32(2.0) * g.r01() - f32(1.0)
+    r = np.sqrt(f32(1.0) - z * z)
+    phi = TAU * g.r01()
+    return [r * _fp("cos", phi), r * _fp("sin", phi), z]
+
+
+def vmf_pdf(kappa, mu, d):
+    """VonMisesFisherPDF (common.glsl.inc:249-254)."""
+    if kappa < EPSILON:
+        return f32(1.0) / (f32(4.0) * PI)
+    c = kappa / ((f32(2.0) * PI) * (f32(1.0) - _fp("exp", f32(-2.0) * kappa)))
+    return c * _fp("exp", kappa * (_dot(mu, d) - f32(1.0)))
+
+
+def parametric(beta, lam):
+    """SampleParametricSpectrum(vec3 Beta, float Lambda)."""
+    x = (beta[0] * lam + beta[1]) * lam + beta[2]
+    return f32(0.5) + x / (f32(2.0) * np.sqrt(f32(1.0) + x * x))
+
+
+def observer(lam):
+    """SampleStandardObserver (spectrum.glsl.inc:10-34)."""
+    def g(mu, lo, hi):
+        t = (lam - f32(mu)) * (f32(lo) if lam < f32(mu) else f32(hi))
+        return _fp("exp", (f32(-0.5) * t) * t)
+    x = (f32(0.362) * g(442.0, 0.0624, 0.0374) + f32(1.056) * g(599.8, 0.0264, 0.0323)) \
+        - f32(0.065) * g(501.1, 0.0490, 0.0382)
+    y = f32(0.821) * g(568.8, 0.0213, 0.0247) + f32(0.286) * g(530.9, 0.0613, 0.0322)
+    z = f32(1.217) * g(437.0, 0.0845, 0.0278) + f32(0.681) * g(459.0, 0.0385, 0.0725)
+    return [x, y, z]
+
+
+class World:
+    """The packed scene: trace tables, materials, textures, atlas, camera, globals."""
+
+    def __init__(self, scene):
+        self.arrays = scene.arrays()
+        packs = scene.packs()
+        self.S = tr.Scene(self.arrays)
+        self.mat = self.arrays["materials"].astype(np.uint32)
+        self.tex = self.arrays["textures"]
+        g = self.arrays["globals"][0]
+        assert int(g["SkyboxTextureIndex"]) == NONE, "scope: no sky texture"
+        assert float(g["SkyboxSamplingProbability"]) == 0.0, "scope: no sky light sampling"
+        self.sky_brightness = f32(g["SkyboxBrightness"])
+        self.kappa = f32(g["SkyboxConcentration"])
+        self.sky_mean = [f32(c) for c in g["SkyboxMeanDirection"]]
+        self.scatter_rate = f32(g["SceneScatterRate"])
+        self.aw, self.ah, layers = packs.atlas_width, packs.atlas_height, packs.atlas_layer_count
+        n = self.aw * self.ah * layers * 4
+        self.atlas = np.frombuffer((C.c_float * n).from_address(packs.atlas), np.float32).reshape(
+            layers, self.ah, self.aw, 4) if n else None
+        for m in self.S.shape_material:
+            assert self.mat[32 * m] == 0, "scope: BasicDiffuse materials only"
+        for t in self.tex:
+            assert int(t["Flags"]) & 1, "scope: nearest-filtered textures only"
+
+    def mfloat(self, m, a):
+        return self.mat[32 * m + a:32 * m + a + 1].view(np.float32)[0]
+
+    def sample_texture(self, index, uv):
+        """SampleTexture, nearest: the texel at floor(u * width), REPEAT."""
+        t = self.tex[index]
+        mn, mx = t["AtlasPlacementMinimum"].astype(np.float32), t["AtlasPlacementMaximum"].astype(np.float32)
+        u = _mix(mn[0], mx[0], _fract(uv[0]))
+        v = _mix(mn[1], mx[1], _fract(uv[1]))
+        i = int(np.floor(u * f32(self.aw))) % self.aw
+        j = int(np.floor(v * f32(self.ah))) % self.ah
+        return self.atlas[int(t["AtlasImageIndex"]), j, i]
+
+    def reflectance(self, m, lam, uv):
+        """MaterialTexturableReflectance(m, BASIC_DIFFUSE_BASE_SPECTRUM = 1)."""
+        beta = [self.mfloat(m, 1), self.mfloat(m, 2), self.mfloat(m, 3)]
+        value = [parametric(beta, l) for l in lam]
+        ti = int(self.mat[32 * m + 4])
+        if ti != NONE:
+            tb = self.sample_texture(ti, uv)
+            value = [value[k] * parametric([tb[0], tb[1], tb[2]], lam[k]) for k in range(4)]
+        return value
+
+
+def new_path(W_, cam, g, x, y, W, H, flags):
+    """GenerateNewPath: the ray (origin, packed velocity) and Lambda0."""
+    if flags & 2:
+        jx = g.r01()
+        jy = g.r01()
+        sx, sy = f32(x) + jx, f32(y) + jy
+    else:
+        sx, sy = f32(x) + f32(0.5), f32(y) + f32(0.5)
+    nx, ny = sx / f32(W), sy / f32(H)
+    model = int(cam["Model"])
+    size = cam["SensorSize"].astype(np.float32)
+    if model in (0, 1):
+        sp = [-size[0] * (nx - f32(0.5)), -size[1] * (f32(0.5) - ny), f32(cam["SensorDistance"])]
+        a = f32(cam["ApertureRadius"])
+        if model == 0:
+            dx, dy = random_point_on_disk(g)
+            o = [a * dx, a * dy, f32(0.0)]
+            v = _normalize([o[0] - sp[0], o[1] - sp[1], o[2] - sp[2]])
+        else:
+            fl = f32(cam["FocalLength"])
+            den = sp[2] - fl
+            op = [(-sp[i] * fl) / den for i in range(3)]
+            dx, dy = random_point_on_disk(g)
+            o = [a * dx, a * dy, f32(0.0)]
+            v = _normalize([op[0] - o[0], op[1] - o[1], op[2] - o[2]])
+    else:
+        phi = (nx - f32(0.5)) * TAU
+        theta = (f32(0.5) - ny) * PI
+        ct, st = _fp("cos", theta), _fp("sin", theta)
+        o = [f32(0.0)] * 3
+        v = [ct * _fp("sin", phi), st, -ct * _fp("cos", phi)]
+    to = cam["Transform"]["To"].astype(np.float32).reshape(16)
+    O = _mat_vec(to, o, 1.0)
+    V = _mat_vec(to, v, 0.0)
+    lam0 = g.r01()
+    return O, int(kat.pack_unit_vector(np.array([V], np.float32))[0]), lam0
+
+
+class Slot:
+    __slots__ = ("O", "PV", "lam0", "thr", "prob", "sample", "active")
+
+    def start(self, O, PV, lam0):
+        self.O, self.PV, self.lam0 = O, PV, lam0
+        self.thr = [f32(1.0)] * 4
+        self.prob = [f32(1.0)] * 4
+        self.sample = [f32(0.0)] * 3
+        self.active = [NONE] * 4
+
+
+def resolve_medium(W_, shape):
+    """ResolveMedium: (priority, ior, absorption, scattering) for diffuse
+    scenes (a BasicDiffuse interior is vacuum: DESIGN.md §2 deviation 2)."""
+    if shape == NONE:
+        return NONE, [f32(1.0)] * 4, [f32(0.0)] * 4, [W_.scatter_rate] * 4
+    return shape, [f32(1.0)] * 4, [f32(0.0)] * 4, [f32(0.0)] * 4
+
+
+def scatter(W_, sl, g, hit, ptp):
+    """Scatter (basic_scatter.glsl:114-310); returns (continues, O', V')."""
+    O = [f32(c) for c in sl.O]
+    V = [f32(c) for c in kat.unpack_unit_vector(np.array([sl.PV], np.uint32))[0]]
+    l0 = sl.lam0
+    lam = [_mix(LAMBDA_MIN, LAMBDA_MAX, l0), _mix(LAMBDA_MIN, LAMBDA_MAX, _fract(l0 + f32(0.25))),
+           _mix(LAMBDA_MIN, LAMBDA_MAX, _fract(l0 + f32(0.50))), _mix(LAMBDA_MIN, LAMBDA_MAX, _fract(l0 + f32(0.75)))]
+    active = min(sl.active)
+    prio, ior, absorb, scat = resolve_medium(W_, active)
+    htime = HIT_TIME_LIMIT if hit is None else hit[1]
+    sl.thr = [sl.thr[k] * _fp("exp", -absorb[k] * htime) for k in range(4)]
+    st = HIT_TIME_LIMIT
+    if scat[0] > 0:
+        st = -_fp("log", g.r01()) / scat[0]
+    if htime >= st:
+        assert st >= HIT_TIME_LIMIT, "scope: no medium scattering"
+        em = [f32(1.0) * parametric([f32(0.0), f32(0.0), f32(100.0)], l) * W_.sky_brightness for l in lam]
+        cluster = ((sl.prob[0] + sl.prob[1]) + sl.prob[2]) + sl.prob[3]
+        e = [em[k] * sl.thr[k] for k in range(4)]
+        obs = [observer(l) for l in lam]
+        xyz = [((obs[0][i] * e[0] + obs[1][i] * e[1]) + obs[2][i] * e[2]) + obs[3][i] * e[3] for i in range(3)]
+        sl.sample = [sl.sample[i] + xyz[i] / cluster for i in range(3)]
+        sl.prob = [f32(0.0)] * 4
+        return False, None, None
+    shape, material, time, pn, ptg, uv = hit[0], hit[2], hit[1], hit[3], hit[4], hit[5]
+    N = [f32(c) for c in kat.unpack_unit_vector(np.array([pn], np.uint32))[0]]
+    TX = [f32(c) for c in kat.unpack_unit_vector(np.array([ptg], np.uint32))[0]]
+    TY = _cross(N, TX)
+    pos = [O[i] + time * V[i] for i in range(3)]
+    out = [-_dot(V, TX), -_dot(V, TY), -_dot(V, N)]
+    exterior = [f32(1.0)] * 4
+    if out[2] > 0:
+        real = prio > shape
+        if real:
+            exterior = ior
+    else:
+        real = prio == shape
+        if real:
+            ext = NONE
+            for a in sl.active:
+                if a != active:
+                    ext = min(ext, a)
+            exterior = resolve_medium(W_, ext)[1]
+    if real:
+        # SampleSurfaceIntegrand, LightProbability = 0: the light choice is
+        # drawn, then BasicDiffuse_SampleBSDF (its In is the path's Out).
+        light_p = f32(0.0)
+        g.r01()
+        d = random_direction(g)
+        inn = _safe_normalize([d[0], d[1], d[2] + f32(1.0)])
+        r = W_.reflectance(material, lam, uv)
+        mpdf = [out[2] / PI] * 4
+        thru = [mpdf[k] * r[k] for k in range(4)]
+        mu = [_dot(W_.sky_mean, TX), _dot(W_.sky_mean, TY), _dot(W_.sky_mean, N)]
+        sky_pdf = vmf_pdf(W_.kappa, mu, inn)
+        prob = [light_p * sky_pdf + (f32(1.0) - light_p) * mpdf[k] for k in range(4)]
+        scale = f32(1.0) / np.fmax(EPSILON, _max4(prob))
+        sl.thr = [sl.thr[k] * (thru[k] * scale) for k in range(4)]
+        sl.prob = [sl.prob[k] * (prob[k] * scale) for k in range(4)]
+    else:
+        inn = [-out[0], -out[1], -out[2]]
+    if inn[2] * out[2] < 0:
+        if out[2] > 0:
+            for i in range(4):
+                if sl.active[i] == NONE:
+                    sl.active[i] = shape
+                    break
+        else:
+            for i in range(4):
+                if sl.active[i] == shape:
+                    sl.active[i] = NONE
+                    break
+    if g.r01() < ptp:
+        return False, None, None
+    sl.prob = [p * (f32(1.0) - ptp) for p in sl.prob]
+    v2 = [(inn[0] * TX[i] + inn[1] * TY[i]) + inn[2] * N[i] for i in range(3)]
+    o2 = [pos[i] + f32(1e-3) * v2[i] for i in range(3)]
+    return bool(_max4(sl.prob) > EPSILON), o2, v2
+
+
+def render(scene, W, H, schedule, flags=3, ptp=0.0, camera=0):
+    """Reset + Run(r) for r in schedule (FrameIndex from 0): (slots, accum)."""
+    W_ = World(scene)
+    cam = W_.arrays["cameras"][camera]
+    ptp = f32(ptp)
+    accum = np.zeros((H, W, 4), np.float32)
+    slots = [[Slot() for _ in range(W)] for _ in range(H)]
+    frame = 0
+    for y in range(H):
+        for x in range(W):
+            g = Rng(x, y, frame)
+            slots[y][x].start(*new_path(W_, cam, g, x, y, W, H, flags))
+    for rounds in schedule:
+        frame += 1
+        for _ in range(rounds):
+            for y in range(H):
+                for x in range(W):
+                    sl = slots[y][x]
+                    V = kat.unpack_unit_vector(np.array([sl.PV], np.uint32))[0]
+                    h = tr.trace(W_.S, sl.O, V, HIT_TIME_LIMIT)
+                    hit = None
+                    if h.shape != tr.SHAPE_INDEX_NONE:
+                        normal, tangent, uv = tr.hit_attributes(W_.S, h)
+                        pn = int(kat.pack_unit_vector(np.array([normal], np.float32))[0])
+                        ptg = int(kat.pack_unit_vector(np.array([tangent], np.float32))[0])
+                        hit = (h.shape, h.time, W_.S.shape_material[h.shape], pn, ptg, uv)
+                    g = Rng(x, y, frame)
+                    cont, o2, v2 = scatter(W_, sl, g, hit, ptp)
+                    if cont:
+                        sl.O = o2
+                        sl.PV = int(kat.pack_unit_vector(np.array([v2], np.float32))[0])
+                    else:
+                        val = [sl.sample[0], sl.sample[1], sl.sample[2], f32(1.0)]
+                        if flags & 1:
+                            val = [accum[y, x, k] + val[k] for k in range(4)]
+                        accum[y, x] = val
+                        sl.start(*new_path(W_, cam, g, x, y, W, H, flags))
+    return slots, accum

@@ -18,74 +18,15 @@ import numpy as np
 import pytest
 
 import fuzz_scenes
-import kat
 import oracle_lib
-
-f32 = np.float32
-TAU = f32(6.283185306)     # common.glsl.inc:7
-PI = f32(3.141592653)      # common.glsl.inc:6
-
-
-def _normalize(v):
-    r = f32(1.0) / np.sqrt((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2])
-    return [v[0] * r, v[1] * r, v[2] * r]
-
-
-def _mat_vec(m, v, w):
-    w = f32(w)
-    return [((m[r] * v[0] + m[4 + r] * v[1]) + m[8 + r] * v[2]) + m[12 + r] * w for r in range(3)]
+import path_restatement as pr
 
 
 def new_path(cam, x, y, W, H, flags, frame):
-    """(origin, packed velocity, lambda0) of GenerateNewPath at pixel (x, y)."""
-    L = oracle_lib.lib()
-    state = kat.seed(x, y, frame)
-
-    def r01():
-        nonlocal state
-        v, state = kat.pcg(state)
-        return f32(v) / f32(4294967296.0)
-
-    def disk():
-        r = np.sqrt(r01())
-        theta = r01() * TAU
-        return r * f32(L.oracle_fp_cos(theta)), r * f32(L.oracle_fp_sin(theta))
-
-    if flags & 2:                                   # RENDER_FLAG_SAMPLE_JITTER
-        jx = r01()
-        jy = r01()
-        sx, sy = f32(x) + jx, f32(y) + jy
-    else:
-        sx, sy = f32(x) + f32(0.5), f32(y) + f32(0.5)
-    nx, ny = sx / f32(W), sy / f32(H)
-    model = int(cam["Model"])
-    size = cam["SensorSize"].astype(np.float32)
-    if model in (0, 1):
-        sp = [-size[0] * (nx - f32(0.5)), -size[1] * (f32(0.5) - ny), f32(cam["SensorDistance"])]
-        if model == 0:
-            dx, dy = disk()
-            a = f32(cam["ApertureRadius"])
-            o = [a * dx, a * dy, f32(0.0)]
-            v = _normalize([o[0] - sp[0], o[1] - sp[1], o[2] - sp[2]])
-        else:
-            fl = f32(cam["FocalLength"])
-            den = sp[2] - fl
-            op = [(-sp[i] * fl) / den for i in range(3)]
-            dx, dy = disk()
-            a = f32(cam["ApertureRadius"])
-            o = [a * dx, a * dy, f32(0.0)]
-            v = _normalize([op[0] - o[0], op[1] - o[1], op[2] - o[2]])
-    else:
-        phi = (nx - f32(0.5)) * TAU
-        theta = (f32(0.5) - ny) * PI
-        ct, st = f32(L.oracle_fp_cos(theta)), f32(L.oracle_fp_sin(theta))
-        o = [f32(0.0)] * 3
-        v = [ct * f32(L.oracle_fp_sin(phi)), st, -ct * f32(L.oracle_fp_cos(phi))]
-    to = cam["Transform"]["To"].astype(np.float32).reshape(16)
-    O = _mat_vec(to, o, 1.0)
-    V = _mat_vec(to, v, 0.0)
-    lam = r01()
-    return np.array(O, np.float32), int(kat.pack_unit_vector(np.array([V], np.float32))[0]), lam
+    """(origin, packed velocity, lambda0) of GenerateNewPath at pixel (x, y)
+    from main's seed (tests/path_restatement.py)."""
+    O, pv, lam = pr.new_path(None, cam, pr.Rng(x, y, frame), x, y, W, H, flags)
+    return np.array(O, np.float32), pv, lam
 
 
 def check(scene, W, H, camera, flags, frame):
