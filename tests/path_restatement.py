@@ -11,18 +11,18 @@ Reset / Run(k) leave in the slot state and the accumulator:
   ResolveMedium                                            basic_scatter.glsl:45-66
   SampleSurfaceIntegrand                                   basic_scatter.glsl:68-109
   BasicDiffuse_SampleBSDF / _EvaluateBSDF                  basic_diffuse.glsl.inc
-  MaterialTexturableReflectance, SampleTexture (nearest)   scene.glsl.inc:180-290
+  MaterialTexturableReflectance, SampleTexture             scene.glsl.inc:180-290
   SampleSkyboxSpectrum / Radiance (no sky texture)         scene.glsl.inc:206-227
   SampleParametricSpectrum, SampleStandardObserver         spectrum.glsl.inc:10-34,169-192
   RandomDirection, RandomPointOnDisk, VonMisesFisherPDF    common.glsl.inc:205-254
 
-Scope: every material BasicDiffuse, textures nearest-filtered, no sky
-texture, SkyboxSamplingProbability 0 (C1's scene).
+Scope: every material BasicDiffuse, no sky texture, SkyboxSamplingProbability
+0 (the scenes of C1 and C3).
 Numerics: DESIGN.md §2's convention (float32, nothing fused, reductions left
 to right, normalize = v * (1 / sqrt(dot)), mix = x*(1-a) + y*a); exp, log,
 sin, cos are the convention's own functions (the oracle's exported pt_exp /
 pt_log / pt_sin / pt_cos), the octahedral packing tests/kat.py's.
-Nearest sampling follows the Vulkan rule i = floor(u * width), REPEAT.
+Texture filtering follows the Vulkan rules (SampleTexture below).
 """
 from __future__ import annotations
 
@@ -157,21 +157,36 @@ class World:
             layers, self.ah, self.aw, 4) if n else None
         for m in self.S.shape_material:
             assert self.mat[32 * m] == 0, "scope: BasicDiffuse materials only"
-        for t in self.tex:
-            assert int(t["Flags"]) & 1, "scope: nearest-filtered textures only"
 
     def mfloat(self, m, a):
         return self.mat[32 * m + a:32 * m + a + 1].view(np.float32)[0]
 
     def sample_texture(self, index, uv):
-        """SampleTexture, nearest: the texel at floor(u * width), REPEAT."""
+        """SampleTexture: textureLod(atlas, (U, V, layer), 0) with REPEAT
+        addressing, by the Vulkan filtering rules in full precision: nearest
+        takes the texel at floor(u * width); linear blends the four texels
+        around u * width - 0.5 with weights (1 - a)(1 - b), a(1 - b),
+        (1 - a)b, ab."""
         t = self.tex[index]
         mn, mx = t["AtlasPlacementMinimum"].astype(np.float32), t["AtlasPlacementMaximum"].astype(np.float32)
         u = _mix(mn[0], mx[0], _fract(uv[0]))
         v = _mix(mn[1], mx[1], _fract(uv[1]))
-        i = int(np.floor(u * f32(self.aw))) % self.aw
-        j = int(np.floor(v * f32(self.ah))) % self.ah
-        return self.atlas[int(t["AtlasImageIndex"]), j, i]
+        layer = self.atlas[int(t["AtlasImageIndex"])]
+        if int(t["Flags"]) & 1:
+            i = int(np.floor(u * f32(self.aw))) % self.aw
+            j = int(np.floor(v * f32(self.ah))) % self.ah
+            return layer[j, i]
+        x = u * f32(self.aw) - f32(0.5)
+        y = v * f32(self.ah) - f32(0.5)
+        fx, fy = np.floor(x), np.floor(y)
+        a, b = x - fx, y - fy
+        i0, j0 = int(fx) % self.aw, int(fy) % self.ah
+        i1, j1 = (i0 + 1) % self.aw, (j0 + 1) % self.ah
+        one = f32(1.0)
+        w = [(one - a) * (one - b), a * (one - b), (one - a) * b, a * b]
+        t00, t10, t01, t11 = layer[j0, i0], layer[j0, i1], layer[j1, i0], layer[j1, i1]
+        return np.array([((w[0] * t00[c] + w[1] * t10[c]) + w[2] * t01[c]) + w[3] * t11[c] for c in range(4)],
+                        np.float32)
 
     def reflectance(self, m, lam, uv):
         """MaterialTexturableReflectance(m, BASIC_DIFFUSE_BASE_SPECTRUM = 1)."""
