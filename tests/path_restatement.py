@@ -1,4 +1,4 @@
-"""A second restatement of the integrator's rounds for BasicDiffuse scenes,
+"""A second restatement of the integrator's rounds for opaque scenes,
 written from the GLSL text apart from oracle/pt_oracle.cpp (test
 infrastructure only; tests/test_path_restatement.py).  With
 tests/trace_restatement.py for Trace() it re-derives, per pixel, what
@@ -11,21 +11,29 @@ Reset / Run(k) leave in the slot state and the accumulator:
   ResolveMedium                                            basic_scatter.glsl:45-66
   SampleSurfaceIntegrand                                   basic_scatter.glsl:68-109
   BasicDiffuse_SampleBSDF / _EvaluateBSDF                  basic_diffuse.glsl.inc
-  MaterialTexturableReflectance, SampleTexture             scene.glsl.inc:180-290
-  SampleSkyboxSpectrum / Radiance (no sky texture)         scene.glsl.inc:206-227
+  BasicMetal_GetParameters / _HasDiracBSDF / _Evaluate / _Sample  basic_metal.glsl.inc
+  MaterialTexturableReflectance / Value, SampleTexture     scene.glsl.inc:180-302
+  SampleSkyboxSpectrum / Radiance (lat-long sky texture)   scene.glsl.inc:206-227
   SampleParametricSpectrum, SampleStandardObserver         spectrum.glsl.inc:10-34,169-192
-  RandomDirection, RandomPointOnDisk, VonMisesFisherPDF    common.glsl.inc:205-254
+  RandomDirection, RandomPointOnDisk, RandomVonMisesFisher,
+  VonMisesFisherPDF, ComputeCoordinateFrame                common.glsl.inc:120-125,205-254
+  GGXRoughnessAlpha / SmithG1 / VisibleNormal / Distribution,
+  SchlickFresnelMetal                                      common.glsl.inc:278-360,425-436
 
-Scope: every material BasicDiffuse, no sky texture, SkyboxSamplingProbability
-0 (the scenes of C1 and C3).
+Scope: BasicDiffuse and BasicMetal materials, no participating medium
+(scatter rate 0); the sky may be textured and light-sampled (the scenes of
+C1, C3 and tests/test_path_restatement.py's metal room).
 Numerics: DESIGN.md §2's convention (float32, nothing fused, reductions left
 to right, normalize = v * (1 / sqrt(dot)), mix = x*(1-a) + y*a); exp, log,
-sin, cos are the convention's own functions (the oracle's exported pt_exp /
-pt_log / pt_sin / pt_cos), the octahedral packing tests/kat.py's.
+sin, cos, atan2, asin are the convention's own functions (the oracle's
+exported pt_exp / pt_log / pt_sin / pt_cos / pt_atan2 / pt_asin), the
+octahedral packing tests/kat.py's; pow(x, 5) and pow(x, 6) are products
+(x^2 x^2) x and (x^2 x^2) x^2, as GPU compilers lower a constant integer power.
 Texture filtering follows the Vulkan rules (SampleTexture below).
 """
 from __future__ import annotations
 
+import collections
 import ctypes as C
 
 import numpy as np
@@ -41,6 +49,7 @@ EPSILON = f32(1e-9)
 HIT_TIME_LIMIT = f32(1048576.0)
 LAMBDA_MIN, LAMBDA_MAX = f32(360.0), f32(830.0)
 NONE = 0xFFFFFFFF
+STATS = collections.Counter()   # which branches a render took (the tests check coverage)
 
 
 def _fp(name, *a):
@@ -117,6 +126,94 @@ def vmf_pdf(kappa, mu, d):
     return c * _fp("exp", kappa * (_dot(mu, d) - f32(1.0)))
 
 
+def coordinate_frame(z):
+    """ComputeCoordinateFrame (common.glsl.inc:120-125)."""
+    v = [f32(1.0), f32(0.0), f32(0.0)] if abs(z[0]) < f32(0.9) else [f32(0.0), f32(1.0), f32(0.0)]
+    x = _normalize(_cross(v, z))
+    return x, _cross(x, z)
+
+
+def random_vmf(g, kappa, mu):
+    """RandomVonMisesFisher(Kappa, Mu) (common.glsl.inc:228-247)."""
+    xi = g.r01()
+    one = f32(1.0)
+    z = one + (one / kappa) * _fp("log", xi + (one - xi) * _fp("exp", f32(-2.0) * kappa))
+    r = np.sqrt(one - z * z)
+    phi = g.r01() * TAU
+    v = [r * _fp("cos", phi), r * _fp("sin", phi), z]
+    mx, my = coordinate_frame(mu)
+    return _safe_normalize([(v[0] * mx[i] + v[1] * my[i]) + v[2] * mu[i] for i in range(3)])
+
+
+def ggx_alpha(rough, aniso):
+    """GGXRoughnessAlpha (common.glsl.inc:281-288)."""
+    s = f32(1.0) - aniso
+    ax = (rough * rough) * np.sqrt(f32(2.0) / (f32(1.0) + s * s))
+    return ax, s * ax
+
+
+def ggx_g1(d, a):
+    """GGXSmithG1 (common.glsl.inc:294-301)."""
+    dsq = [d[0] * d[0], d[1] * d[1], d[2] * d[2]]
+    if dsq[2] < EPSILON:
+        return f32(0.0)
+    t = (a[0] * a[0] * dsq[0] + a[1] * a[1] * dsq[1]) / dsq[2]
+    return f32(2.0) / (f32(1.0) + np.sqrt(f32(1.0) + t))
+
+
+def ggx_visible_normal(d, a, u1, u2):
+    """GGXVisibleNormal (common.glsl.inc:306-345)."""
+    one = f32(1.0)
+    vz = _safe_normalize([a[0] * d[0], a[1] * d[1], d[2]])
+    lsq = vz[0] * vz[0] + vz[1] * vz[1]
+    if lsq > 0:
+        ln = np.sqrt(lsq)
+        vx = [-vz[1] / ln, vz[0] / ln, f32(0.0) / ln]
+    else:
+        vx = [one, f32(0.0), f32(0.0)]
+    vy = _cross(vz, vx)
+    r = np.sqrt(u1)
+    phi = TAU * u2
+    s = f32(0.5) * (one + vz[2])
+    tx = r * _fp("cos", phi)
+    ty = (one - s) * np.sqrt(one - tx * tx) + (s * r) * _fp("sin", phi)
+    tz = np.sqrt(np.fmax(f32(0.0), (one - tx * tx) - ty * ty))
+    n = [(tx * vx[i] + ty * vy[i]) + tz * vz[i] for i in range(3)]
+    return _safe_normalize([a[0] * n[0], a[1] * n[1], np.fmax(f32(0.0), n[2])])
+
+
+def ggx_distribution(n, a):
+    """GGXDistribution (common.glsl.inc:349-354)."""
+    inv = [f32(1.0) / a[0], f32(1.0) / a[1]]
+    b = (n[0] * n[0] * (inv[0] * inv[0]) + n[1] * n[1] * (inv[1] * inv[1])) + n[2] * n[2] * f32(1.0)
+    return f32(1.0) / ((((PI * a[0]) * a[1]) * b) * b)
+
+
+def _pow5(x):
+    x2 = x * x
+    return (x2 * x2) * x
+
+
+def _pow6(x):
+    x2 = x * x
+    return (x2 * x2) * x2
+
+
+def schlick_fresnel_metal(base, spec, c):
+    """SchlickFresnelMetal, F82-tint (common.glsl.inc:425-436)."""
+    one = f32(1.0)
+    cmax = one / f32(7.0)
+    den = cmax * _pow6(one - cmax)
+    nom = c * _pow6(one - c)
+    out = []
+    for k in range(4):
+        fs = base[k] + (one - base[k]) * _pow5(one - c)
+        fsm = base[k] + (one - base[k]) * _pow5(one - cmax)
+        fm = spec[k] * fsm
+        out.append(fs - (nom / den) * (fsm - fm))
+    return out
+
+
 def parametric(beta, lam):
     """SampleParametricSpectrum(vec3 Beta, float Lambda)."""
     x = (beta[0] * lam + beta[1]) * lam + beta[2]
@@ -145,8 +242,8 @@ class World:
         self.mat = self.arrays["materials"].astype(np.uint32)
         self.tex = self.arrays["textures"]
         g = self.arrays["globals"][0]
-        assert int(g["SkyboxTextureIndex"]) == NONE, "scope: no sky texture"
-        assert float(g["SkyboxSamplingProbability"]) == 0.0, "scope: no sky light sampling"
+        self.sky_index = int(g["SkyboxTextureIndex"])
+        self.light_p = f32(g["SkyboxSamplingProbability"])
         self.sky_brightness = f32(g["SkyboxBrightness"])
         self.kappa = f32(g["SkyboxConcentration"])
         self.sky_mean = [f32(c) for c in g["SkyboxMeanDirection"]]
@@ -156,7 +253,7 @@ class World:
         self.atlas = np.frombuffer((C.c_float * n).from_address(packs.atlas), np.float32).reshape(
             layers, self.ah, self.aw, 4) if n else None
         for m in self.S.shape_material:
-            assert self.mat[32 * m] == 0, "scope: BasicDiffuse materials only"
+            assert self.mat[32 * m] in (0, 1), "scope: BasicDiffuse and BasicMetal materials only"
 
     def mfloat(self, m, a):
         return self.mat[32 * m + a:32 * m + a + 1].view(np.float32)[0]
@@ -188,15 +285,33 @@ class World:
         return np.array([((w[0] * t00[c] + w[1] * t10[c]) + w[2] * t01[c]) + w[3] * t11[c] for c in range(4)],
                         np.float32)
 
-    def reflectance(self, m, lam, uv):
-        """MaterialTexturableReflectance(m, BASIC_DIFFUSE_BASE_SPECTRUM = 1)."""
-        beta = [self.mfloat(m, 1), self.mfloat(m, 2), self.mfloat(m, 3)]
+    def reflectance(self, m, lam, uv, a=1):
+        """MaterialTexturableReflectance(m, a) (BASE_SPECTRUM = 1, metal SPECULAR_SPECTRUM = 5)."""
+        beta = [self.mfloat(m, a), self.mfloat(m, a + 1), self.mfloat(m, a + 2)]
         value = [parametric(beta, l) for l in lam]
-        ti = int(self.mat[32 * m + 4])
+        ti = int(self.mat[32 * m + a + 3])
         if ti != NONE:
             tb = self.sample_texture(ti, uv)
             value = [value[k] * parametric([tb[0], tb[1], tb[2]], lam[k]) for k in range(4)]
         return value
+
+    def value(self, m, a, uv):
+        """MaterialTexturableValue (scene.glsl.inc:292-302)."""
+        v = self.mfloat(m, a)
+        ti = int(self.mat[32 * m + a + 1])
+        if ti != NONE:
+            v = v * self.sample_texture(ti, uv)[0]
+        return v
+
+    def sky_spectrum(self, d):
+        """SampleSkyboxSpectrum (scene.glsl.inc:206-218): (beta, intensity)."""
+        if self.sky_index == NONE:
+            return [f32(0.0), f32(0.0), f32(100.0), f32(1.0)]
+        phi = _fp("atan2", d[1], d[0])
+        theta = _fp("asin", d[2])
+        u = f32(0.5) + phi / TAU
+        v = f32(0.5) + theta / PI
+        return list(self.sample_texture(self.sky_index, [u, v]))
 
 
 def new_path(W_, cam, g, x, y, W, H, flags):
@@ -256,6 +371,80 @@ def resolve_medium(W_, shape):
     return shape, [f32(1.0)] * 4, [f32(0.0)] * 4, [f32(0.0)] * 4
 
 
+def metal_parameters(W_, m, lam, uv):
+    """BasicMetal_GetParameters: base, specular, alpha, rough."""
+    base = W_.reflectance(m, lam, uv, 1)
+    spec = W_.reflectance(m, lam, uv, 5)
+    a = ggx_alpha(W_.value(m, 9, uv), W_.value(m, 11, uv))
+    return base, spec, a, bool(a[0] * a[1] > EPSILON)
+
+
+def evaluate_bsdf(W_, m, lam, uv, In, Out):
+    """MaterialEvaluateBSDF (In = the path's Out, Out = the new In):
+    (ok, throughput, probability)."""
+    if W_.mat[32 * m] == 0:
+        r = W_.reflectance(m, lam, uv)
+        p = In[2] / PI
+        return True, [p * r[k] for k in range(4)], [p] * 4
+    base, spec, a, rough = metal_parameters(W_, m, lam, uv)
+    if In[2] <= 0 or Out[2] <= 0 or not rough:
+        return False, None, None
+    h = _safe_normalize([In[i] + Out[i] for i in range(3)])
+    gm = ggx_g1(In, a)
+    d = ggx_distribution(h, a)
+    p = (gm * d) / (f32(4.0) * In[2])
+    gs = ggx_g1(Out, a)
+    f = schlick_fresnel_metal(base, spec, _dot(In, h))
+    return True, [(p * gs) * f[k] for k in range(4)], [p] * 4
+
+
+def sample_bsdf(W_, g, m, lam, uv, In):
+    """MaterialSampleBSDF: (ok, Out, throughput, probability)."""
+    if W_.mat[32 * m] == 0:
+        d = random_direction(g)
+        Out = _safe_normalize([d[0], d[1], d[2] + f32(1.0)])
+        return (True, Out) + evaluate_bsdf(W_, m, lam, uv, In, Out)[1:]
+    base, spec, a, rough = metal_parameters(W_, m, lam, uv)
+    if In[2] <= 0:
+        return False, None, None, None
+    u1 = g.r01()
+    u2 = g.r01()
+    n = ggx_visible_normal(In, a, u1, u2)
+    c = min(_dot(n, In), f32(1.0))
+    Out = [(f32(2.0) * c) * n[i] - In[i] for i in range(3)]
+    if Out[2] <= 0:
+        return False, None, None, None
+    p = f32(1.0)
+    if rough:
+        gm = ggx_g1(In, a)
+        d = ggx_distribution(n, a)
+        p = p * ((gm * d) / (f32(4.0) * In[2]))
+    gs = ggx_g1(Out, a)
+    f = schlick_fresnel_metal(base, spec, c)
+    return True, Out, [(p * gs) * f[k] for k in range(4)], [p] * 4
+
+
+def sample_surface_integrand(W_, g, m, lam, uv, TX, TY, N, out):
+    """SampleSurfaceIntegrand (basic_scatter.glsl:68-109): (ok, In, throughput, probability)."""
+    dirac = W_.mat[32 * m] == 1 and W_.value(m, 9, uv) < f32(1e-3)
+    light_p = f32(0.0) if dirac else W_.light_p
+    mu = [_dot(W_.sky_mean, TX), _dot(W_.sky_mean, TY), _dot(W_.sky_mean, N)]
+    STATS["dirac" if dirac else ("metal" if W_.mat[32 * m] == 1 else "diffuse")] += 1
+    if g.r01() < light_p:
+        STATS["light"] += 1
+        inn = random_vmf(g, W_.kappa, mu)
+        if inn[2] < 0:
+            return False, None, None, None
+        ok, thru, mpdf = evaluate_bsdf(W_, m, lam, uv, out, inn)
+    else:
+        ok, inn, thru, mpdf = sample_bsdf(W_, g, m, lam, uv, out)
+    if not ok:
+        return False, None, None, None
+    sky_pdf = vmf_pdf(W_.kappa, mu, inn)
+    one = f32(1.0)
+    return True, inn, thru, [light_p * sky_pdf + (one - light_p) * mpdf[k] for k in range(4)]
+
+
 def scatter(W_, sl, g, hit, ptp):
     """Scatter (basic_scatter.glsl:114-310); returns (continues, O', V')."""
     O = [f32(c) for c in sl.O]
@@ -272,7 +461,8 @@ def scatter(W_, sl, g, hit, ptp):
         st = -_fp("log", g.r01()) / scat[0]
     if htime >= st:
         assert st >= HIT_TIME_LIMIT, "scope: no medium scattering"
-        em = [f32(1.0) * parametric([f32(0.0), f32(0.0), f32(100.0)], l) * W_.sky_brightness for l in lam]
+        sp = W_.sky_spectrum(V)
+        em = [sp[3] * parametric(sp[:3], l) * W_.sky_brightness for l in lam]
         cluster = ((sl.prob[0] + sl.prob[1]) + sl.prob[2]) + sl.prob[3]
         e = [em[k] * sl.thr[k] for k in range(4)]
         obs = [observer(l) for l in lam]
@@ -300,18 +490,9 @@ def scatter(W_, sl, g, hit, ptp):
                     ext = min(ext, a)
             exterior = resolve_medium(W_, ext)[1]
     if real:
-        # SampleSurfaceIntegrand, LightProbability = 0: the light choice is
-        # drawn, then BasicDiffuse_SampleBSDF (its In is the path's Out).
-        light_p = f32(0.0)
-        g.r01()
-        d = random_direction(g)
-        inn = _safe_normalize([d[0], d[1], d[2] + f32(1.0)])
-        r = W_.reflectance(material, lam, uv)
-        mpdf = [out[2] / PI] * 4
-        thru = [mpdf[k] * r[k] for k in range(4)]
-        mu = [_dot(W_.sky_mean, TX), _dot(W_.sky_mean, TY), _dot(W_.sky_mean, N)]
-        sky_pdf = vmf_pdf(W_.kappa, mu, inn)
-        prob = [light_p * sky_pdf + (f32(1.0) - light_p) * mpdf[k] for k in range(4)]
+        ok, inn, thru, prob = sample_surface_integrand(W_, g, material, lam, uv, TX, TY, N, out)
+        if not ok:
+            return False, None, None
         scale = f32(1.0) / np.fmax(EPSILON, _max4(prob))
         sl.thr = [sl.thr[k] * (thru[k] * scale) for k in range(4)]
         sl.prob = [sl.prob[k] * (prob[k] * scale) for k in range(4)]
