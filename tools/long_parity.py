@@ -4,7 +4,10 @@ re-sorts, the path population turned over many times; round 3 ran 700
 rounds, about a 256-spp frame), every slot's state and every accumulated
 pixel compared with the CPU oracle bit for bit.  Prints one JSON line.
 
-usage: python tools/long_parity.py [CONFIG] [ROUNDS]"""
+A random scene of tests/fuzz_scenes.py runs as CONFIG "fuzz:SEED" at
+320x240 with the seed's RenderFlags, roulette and camera.
+
+usage: python tools/long_parity.py [CONFIG | fuzz:SEED] [ROUNDS]"""
 import json
 import sys
 import time
@@ -21,11 +24,17 @@ import oracle_lib  # noqa: E402
 
 def main():
     pt = load()
-    cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "3"
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 64
-    s = pt.Scene.config(cfg)
-    info = s.info
-    W, H = info.width, info.height
+    if cfg.startswith("fuzz:"):
+        import fuzz_scenes
+        s, st = fuzz_scenes.build(pt, int(cfg[5:]))
+        W, H, flags, ptp, camera = 320, 240, st["flags"], st["termination"], st["camera"]
+    else:
+        cfg = int(cfg)
+        s = pt.Scene.config(cfg)
+        info = s.info
+        W, H, flags, ptp, camera = info.width, info.height, info.render_flags, info.termination_probability, 0
     dev = pt.Device(0)
     ds = pt.DeviceScene(dev)
     ds.update(s)
@@ -34,8 +43,9 @@ def main():
     o = oracle_lib.OracleRenderer(s.packs(), W, H)
     t0 = time.time()
     for x in (r, o):
-        x.RenderFlags = info.render_flags
-        x.PathTerminationProbability = info.termination_probability
+        x.RenderFlags = flags
+        x.PathTerminationProbability = ptp
+        x.CameraIndex = camera
         x.reset()
         x.run(2)
     for i in range(rounds - 2):
