@@ -20,9 +20,15 @@ Reset / Run(k) leave in the slot state and the accumulator:
   GGXRoughnessAlpha / SmithG1 / VisibleNormal / Distribution,
   SchlickFresnelMetal                                      common.glsl.inc:278-360,425-436
 
-Scope: BasicDiffuse and BasicMetal materials, no participating medium
-(scatter rate 0); the sky may be textured and light-sampled (the scenes of
-C1, C3 and tests/test_path_restatement.py's metal room).
+  BasicTranslucent_GetParameters / _LoadMedium / _HasDiracBSDF / _Evaluate /
+  _SampleBSDF                                              basic_translucent.glsl.inc
+  CauchyEmpiricalIOR, ComputeCosThetaRefracted, FresnelDielectric  common.glsl.inc:356-420
+  SampleDirectionHG (medium scattering in Scatter)         common.glsl.inc:256-276
+
+Scope: the three basic materials (no OpenPBR surface), nested media with
+absorption and scattering, a scattering scene medium; the sky may be
+textured and light-sampled (C1, C2, C3, a metal room, the fuzz scenes
+without OpenPBR).
 Numerics: DESIGN.md §2's convention (float32, nothing fused, reductions left
 to right, normalize = v * (1 / sqrt(dot)), mix = x*(1-a) + y*a); exp, log,
 sin, cos, atan2, asin are the convention's own functions (the oracle's
@@ -214,6 +220,50 @@ def schlick_fresnel_metal(base, spec, c):
     return out
 
 
+def cauchy_ior(base, abbe, lam):
+    """CauchyEmpiricalIOR (common.glsl.inc:360-371)."""
+    lc, ld, lf = f32(656.3), f32(587.6), f32(486.1)
+    one = f32(1.0)
+    b = (base - one) / (abbe * (one / (lf * lf) - one / (lc * lc)))
+    a = base - b / (ld * ld)
+    return [a + b / (l * l) for l in lam]
+
+
+def cos_refracted(eta, c):
+    """ComputeCosThetaRefracted (common.glsl.inc:378-382)."""
+    c2 = f32(1.0) - (eta * eta) * (f32(1.0) - c * c)
+    return -np.sign(c) * np.sqrt(np.fmax(c2, f32(0.0)))
+
+
+def fresnel_dielectric(eta, c1, c2):
+    """FresnelDielectric(Eta, CosTheta1, CosTheta2) (common.glsl.inc:395-403)."""
+    ks = eta * c1
+    rs = (ks + c2) / (ks - c2)
+    kp = eta * c2
+    rp = (kp + c1) / (kp - c1)
+    return f32(0.5) * (rs * rs + rp * rp)
+
+
+def fresnel4(eta, c1, c2=None):
+    """The vec4 overloads (common.glsl.inc:406-420)."""
+    if c2 is None:
+        c2 = [cos_refracted(eta[k], c1[k]) for k in range(4)]
+    return [fresnel_dielectric(eta[k], c1[k], c2[k]) for k in range(4)]
+
+
+def sample_direction_hg(g_, u1, u2):
+    """SampleDirectionHG (common.glsl.inc:259-276)."""
+    one, two = f32(1.0), f32(2.0)
+    if abs(g_) < f32(1e-3):
+        z = one - two * u1
+    else:
+        s = (one - g_ * g_) / ((one + g_) - (two * g_) * u1)
+        z = -((one + g_ * g_) - s * s) / (two * g_)
+    r = np.sqrt(one - z * z)
+    phi = u2 * TAU
+    return [r * _fp("cos", phi), r * _fp("sin", phi), z]
+
+
 def parametric(beta, lam):
     """SampleParametricSpectrum(vec3 Beta, float Lambda)."""
     x = (beta[0] * lam + beta[1]) * lam + beta[2]
@@ -253,7 +303,7 @@ class World:
         self.atlas = np.frombuffer((C.c_float * n).from_address(packs.atlas), np.float32).reshape(
             layers, self.ah, self.aw, 4) if n else None
         for m in self.S.shape_material:
-            assert self.mat[32 * m] in (0, 1), "scope: BasicDiffuse and BasicMetal materials only"
+            assert self.mat[32 * m] in (0, 1, 2), "scope: the basic materials only"
 
     def mfloat(self, m, a):
         return self.mat[32 * m + a:32 * m + a + 1].view(np.float32)[0]
@@ -363,12 +413,24 @@ class Slot:
         self.active = [NONE] * 4
 
 
-def resolve_medium(W_, shape):
-    """ResolveMedium: (priority, ior, absorption, scattering) for diffuse
-    scenes (a BasicDiffuse interior is vacuum: DESIGN.md §2 deviation 2)."""
+def resolve_medium(W_, shape, lam):
+    """ResolveMedium (basic_scatter.glsl:45-66): (priority, ior, absorption,
+    scattering, anisotropy); BasicTranslucent_LoadMedium for glass, vacuum for
+    the other materials (DESIGN.md §2 deviation 2)."""
+    zero = [f32(0.0)] * 4
     if shape == NONE:
-        return NONE, [f32(1.0)] * 4, [f32(0.0)] * 4, [W_.scatter_rate] * 4
-    return shape, [f32(1.0)] * 4, [f32(0.0)] * 4, [f32(0.0)] * 4
+        return NONE, [f32(1.0)] * 4, zero, [W_.scatter_rate] * 4, f32(0.0)
+    m = W_.S.shape_material[shape]
+    if W_.mat[32 * m] != 2:
+        return shape, [f32(1.0)] * 4, zero, zero, f32(0.0)
+    ior = cauchy_ior(W_.mfloat(m, 1), W_.mfloat(m, 2), lam)
+    depth = W_.mfloat(m, 10)
+    if depth > 0:
+        tr_ = [parametric([W_.mfloat(m, 7), W_.mfloat(m, 8), W_.mfloat(m, 9)], l) for l in lam]
+        sc = [parametric([W_.mfloat(m, 11), W_.mfloat(m, 12), W_.mfloat(m, 13)], l) / depth for l in lam]
+        ext = [-_fp("log", t) / depth for t in tr_]
+        return shape, ior, [np.fmax(ext[k] - sc[k], f32(0.0)) for k in range(4)], sc, W_.mfloat(m, 14)
+    return shape, ior, zero, zero, f32(0.0)
 
 
 def metal_parameters(W_, m, lam, uv):
@@ -379,9 +441,11 @@ def metal_parameters(W_, m, lam, uv):
     return base, spec, a, bool(a[0] * a[1] > EPSILON)
 
 
-def evaluate_bsdf(W_, m, lam, uv, In, Out):
+def evaluate_bsdf(W_, m, lam, uv, exterior, In, Out):
     """MaterialEvaluateBSDF (In = the path's Out, Out = the new In):
     (ok, throughput, probability)."""
+    if W_.mat[32 * m] == 2:
+        return translucent_evaluate(W_, m, lam, uv, exterior, In, Out)
     if W_.mat[32 * m] == 0:
         r = W_.reflectance(m, lam, uv)
         p = In[2] / PI
@@ -398,12 +462,14 @@ def evaluate_bsdf(W_, m, lam, uv, In, Out):
     return True, [(p * gs) * f[k] for k in range(4)], [p] * 4
 
 
-def sample_bsdf(W_, g, m, lam, uv, In):
+def sample_bsdf(W_, g, m, lam, uv, exterior, In):
     """MaterialSampleBSDF: (ok, Out, throughput, probability)."""
+    if W_.mat[32 * m] == 2:
+        return translucent_sample(W_, g, m, lam, uv, exterior, In)
     if W_.mat[32 * m] == 0:
         d = random_direction(g)
         Out = _safe_normalize([d[0], d[1], d[2] + f32(1.0)])
-        return (True, Out) + evaluate_bsdf(W_, m, lam, uv, In, Out)[1:]
+        return (True, Out) + evaluate_bsdf(W_, m, lam, uv, exterior, In, Out)[1:]
     base, spec, a, rough = metal_parameters(W_, m, lam, uv)
     if In[2] <= 0:
         return False, None, None, None
@@ -424,20 +490,108 @@ def sample_bsdf(W_, g, m, lam, uv, In):
     return True, Out, [(p * gs) * f[k] for k in range(4)], [p] * 4
 
 
-def sample_surface_integrand(W_, g, m, lam, uv, TX, TY, N, out):
+def translucent_parameters(W_, m, lam, uv, In, exterior):
+    """BasicTranslucent_GetParameters: relative IOR, alpha, rough."""
+    interior = cauchy_ior(W_.mfloat(m, 1), W_.mfloat(m, 2), lam)
+    if In[2] < 0:
+        rel = [interior[k] / exterior[k] for k in range(4)]
+    else:
+        rel = [exterior[k] / interior[k] for k in range(4)]
+    a = ggx_alpha(W_.value(m, 3, uv), W_.value(m, 5, uv))
+    return rel, a, bool(a[0] * a[1] > EPSILON)
+
+
+def _refraction_terms(In, Out, rel, a, cin, cout, d0=None, n0=None):
+    """The rough refraction probability D (1 - F) Gm J |cos / In.z| shared
+    by evaluate and sample (basic_translucent.glsl.inc)."""
+    f = fresnel4(rel, cin, cout)
+    d = [f32(0.0)] * 4
+    for k in range(4):
+        if k == 0 and d0 is not None:
+            d[0] = d0
+        elif cin[k] * cout[k] < 0:
+            d[k] = ggx_distribution(n0[k], a)
+    gm = ggx_g1(In, a)
+    one = f32(1.0)
+    out = []
+    for k in range(4):
+        t = cin[k] * rel[k] + cout[k]
+        j = abs(cout[k]) / (t * t)
+        out.append((((d[k] * (one - f[k])) * gm) * j) * abs(cin[k] / In[2]))
+    return out
+
+
+def translucent_evaluate(W_, m, lam, uv, exterior, In, Out):
+    rel, a, rough = translucent_parameters(W_, m, lam, uv, In, exterior)
+    if not rough:
+        return True, [f32(0.0)] * 4, [f32(0.0)] * 4
+    gm = ggx_g1(In, a)
+    if In[2] * Out[2] > 0:
+        h = _safe_normalize([Out[i] + In[i] for i in range(3)])
+        c = _dot(h, In)
+        f = fresnel4(rel, [c] * 4)
+        d = ggx_distribution(h, a)
+        p = [((f[k] * gm) * d) / (f32(4.0) * In[2]) for k in range(4)]
+    else:
+        hs = [_safe_normalize([Out[i] + In[i] * rel[k] for i in range(3)]) for k in range(4)]
+        cin = [_dot(In, hs[k]) for k in range(4)]
+        cout = [_dot(Out, hs[k]) for k in range(4)]
+        p = _refraction_terms(In, Out, rel, a, cin, cout, n0=hs)
+    gs = ggx_g1(Out, a)
+    return True, [p[k] * gs for k in range(4)], p
+
+
+def translucent_sample(W_, g, m, lam, uv, exterior, In):
+    rel, a, rough = translucent_parameters(W_, m, lam, uv, In, exterior)
+    u1 = g.r01()
+    u2 = g.r01()
+    sg = np.sign(In[2])
+    n = ggx_visible_normal([In[0] * sg, In[1] * sg, In[2] * sg], a, u1, u2)
+    c = np.clip(_dot(n, In), f32(-1.0), f32(1.0))
+    cr = cos_refracted(rel[0], c)
+    refl = fresnel_dielectric(rel[0], c, cr)
+    if g.r01() < refl:
+        STATS["reflect"] += 1
+        Out = [(f32(2.0) * c) * n[i] - In[i] for i in range(3)]
+        if Out[2] * In[2] <= 0:
+            return False, None, None, None
+        p = fresnel4(rel, [c] * 4)
+        if rough:
+            gm = ggx_g1(In, a)
+            d = ggx_distribution(n, a)
+            p = [p[k] * ((gm * d) / (f32(4.0) * abs(In[2]))) for k in range(4)]
+        gs = ggx_g1(Out, a)
+        return True, Out, [p[k] * gs for k in range(4)], p
+    STATS["refract"] += 1
+    Out = [(cr + rel[0] * c) * n[i] - rel[0] * In[i] for i in range(3)]
+    if Out[2] * In[2] >= 0:
+        return False, None, None, None
+    if rough:
+        ns = [n] + [_safe_normalize([Out[i] + In[i] * rel[k] for i in range(3)]) for k in (1, 2, 3)]
+        cin = [c] + [_dot(In, ns[k]) for k in (1, 2, 3)]
+        cout = [cr] + [_dot(Out, ns[k]) for k in (1, 2, 3)]
+        p = _refraction_terms(In, Out, rel, a, cin, cout, d0=ggx_distribution(n, a), n0=ns)
+    else:
+        p = [f32(1.0) - refl, f32(0.0), f32(0.0), f32(0.0)]
+    gs = ggx_g1(Out, a)
+    return True, Out, [p[k] * gs for k in range(4)], p
+
+
+def sample_surface_integrand(W_, g, m, lam, uv, exterior, TX, TY, N, out):
     """SampleSurfaceIntegrand (basic_scatter.glsl:68-109): (ok, In, throughput, probability)."""
-    dirac = W_.mat[32 * m] == 1 and W_.value(m, 9, uv) < f32(1e-3)
+    typ = int(W_.mat[32 * m])
+    dirac = (typ == 1 and W_.value(m, 9, uv) < f32(1e-3)) or (typ == 2 and W_.value(m, 3, uv) < f32(1e-3))
     light_p = f32(0.0) if dirac else W_.light_p
     mu = [_dot(W_.sky_mean, TX), _dot(W_.sky_mean, TY), _dot(W_.sky_mean, N)]
-    STATS["dirac" if dirac else ("metal" if W_.mat[32 * m] == 1 else "diffuse")] += 1
+    STATS[("diffuse", "metal", "glass")[typ] + ("_dirac" if dirac else "")] += 1
     if g.r01() < light_p:
         STATS["light"] += 1
         inn = random_vmf(g, W_.kappa, mu)
         if inn[2] < 0:
             return False, None, None, None
-        ok, thru, mpdf = evaluate_bsdf(W_, m, lam, uv, out, inn)
+        ok, thru, mpdf = evaluate_bsdf(W_, m, lam, uv, exterior, out, inn)
     else:
-        ok, inn, thru, mpdf = sample_bsdf(W_, g, m, lam, uv, out)
+        ok, inn, thru, mpdf = sample_bsdf(W_, g, m, lam, uv, exterior, out)
     if not ok:
         return False, None, None, None
     sky_pdf = vmf_pdf(W_.kappa, mu, inn)
@@ -453,14 +607,27 @@ def scatter(W_, sl, g, hit, ptp):
     lam = [_mix(LAMBDA_MIN, LAMBDA_MAX, l0), _mix(LAMBDA_MIN, LAMBDA_MAX, _fract(l0 + f32(0.25))),
            _mix(LAMBDA_MIN, LAMBDA_MAX, _fract(l0 + f32(0.50))), _mix(LAMBDA_MIN, LAMBDA_MAX, _fract(l0 + f32(0.75)))]
     active = min(sl.active)
-    prio, ior, absorb, scat = resolve_medium(W_, active)
+    prio, ior, absorb, scat, aniso = resolve_medium(W_, active, lam)
     htime = HIT_TIME_LIMIT if hit is None else hit[1]
     sl.thr = [sl.thr[k] * _fp("exp", -absorb[k] * htime) for k in range(4)]
     st = HIT_TIME_LIMIT
     if scat[0] > 0:
         st = -_fp("log", g.r01()) / scat[0]
+    if htime >= st and st < HIT_TIME_LIMIT:
+        STATS["medium" if abs(aniso) < f32(1e-3) else "medium_hg"] += 1
+        o2 = [O[i] + V[i] * st for i in range(3)]
+        X, Y = coordinate_frame(V)
+        u1 = g.r01()
+        u2 = g.r01()
+        sd = sample_direction_hg(aniso, u1, u2)
+        dens = [scat[k] * _fp("exp", -scat[k] * st) for k in range(4)]
+        mx = np.fmax(EPSILON, _max4(dens))
+        dens = [d / mx for d in dens]
+        sl.thr = [sl.thr[k] * dens[k] for k in range(4)]
+        sl.prob = [sl.prob[k] * dens[k] for k in range(4)]
+        v2 = _normalize([(X[i] * sd[0] + Y[i] * sd[1]) + V[i] * sd[2] for i in range(3)])
+        return bool(_max4(sl.prob) > EPSILON), o2, v2
     if htime >= st:
-        assert st >= HIT_TIME_LIMIT, "scope: no medium scattering"
         sp = W_.sky_spectrum(V)
         em = [sp[3] * parametric(sp[:3], l) * W_.sky_brightness for l in lam]
         cluster = ((sl.prob[0] + sl.prob[1]) + sl.prob[2]) + sl.prob[3]
@@ -488,9 +655,9 @@ def scatter(W_, sl, g, hit, ptp):
             for a in sl.active:
                 if a != active:
                     ext = min(ext, a)
-            exterior = resolve_medium(W_, ext)[1]
+            exterior = resolve_medium(W_, ext, lam)[1]
     if real:
-        ok, inn, thru, prob = sample_surface_integrand(W_, g, material, lam, uv, TX, TY, N, out)
+        ok, inn, thru, prob = sample_surface_integrand(W_, g, material, lam, uv, exterior, TX, TY, N, out)
         if not ok:
             return False, None, None
         scale = f32(1.0) / np.fmax(EPSILON, _max4(prob))
@@ -515,6 +682,19 @@ def scatter(W_, sl, g, hit, ptp):
     v2 = [(inn[0] * TX[i] + inn[1] * TY[i]) + inn[2] * N[i] for i in range(3)]
     o2 = [pos[i] + f32(1e-3) * v2[i] for i in range(3)]
     return bool(_max4(sl.prob) > EPSILON), o2, v2
+
+
+def store_active(sl):
+    """StorePathVertexData / LoadPath's active-shape words (basic.glsl.inc:
+    184-193, 214-215): (A[1] << 16) | A[0] in 32 bits, so an empty slot 0
+    (SHAPE_INDEX_NONE = 0xFFFFFFFF) ORs slot 1 away -- kept as written."""
+    a = sl.active
+    words = [(((a[1] << 16) | a[0]) & 0xFFFFFFFF), (((a[3] << 16) | a[2]) & 0xFFFFFFFF)]
+    out = []
+    for w in words:
+        for v in (w & 0xFFFF, w >> 16):
+            out.append(NONE if v == 0xFFFF else v)
+    sl.active = out
 
 
 def render(scene, W, H, schedule, flags=3, ptp=0.0, camera=0):
@@ -548,6 +728,7 @@ def render(scene, W, H, schedule, flags=3, ptp=0.0, camera=0):
                     if cont:
                         sl.O = o2
                         sl.PV = int(kat.pack_unit_vector(np.array([v2], np.float32))[0])
+                        store_active(sl)
                     else:
                         val = [sl.sample[0], sl.sample[1], sl.sample[2], f32(1.0)]
                         if flags & 1:

@@ -1,17 +1,22 @@
 """Cross-check of the oracle's rounds against a second restatement written
 from the GLSL text apart from it (tests/path_restatement.py, with
-tests/trace_restatement.py for Trace): C1's scene (diffuse sphere and plane
-with a nearest-filtered checker texture, constant sky) and C3's (the room
-mesh with its bilinear-filtered texture) after Reset, Run(2), Run(1), Run(1)
--- every slot's ray, Lambda0, throughput, probability, sample and
-active-shape stack, and every accumulated pixel, bit for bit; with and
-without jitter, with Russian roulette, accumulate and overwrite.  A metal
-room adds the metal BSDF, sky light sampling and the textured sky."""
+tests/trace_restatement.py for Trace): after Reset, Run(2), Run(1), Run(1),
+every slot's ray, Lambda0, throughput, probability, sample and active-shape
+words, and every accumulated pixel, bit for bit -- on C1 (diffuse sphere and
+plane, nearest checker, constant sky), C2 (glass, metal, HDR sky sampled by
+the vMF lobe), C3 (the room mesh, bilinear texture), a metal room, and the
+random fuzz scenes without OpenPBR (rough and smooth glass with dispersion,
+nested and scattering media, a scattering scene medium, textured roughness,
+every camera model); with and without jitter, with Russian roulette,
+accumulate and overwrite."""
 from __future__ import annotations
+
+import collections
 
 import numpy as np
 import pytest
 
+import fuzz_scenes
 import oracle_lib
 import path_restatement as pr
 
@@ -20,14 +25,14 @@ def bits(a):
     return np.asarray(a, np.float32).view(np.uint32)
 
 
-@pytest.mark.parametrize("flags,ptp", [(3, 0.0), (1, 0.0), (3, 0.3), (2, 0.0)])
-def test_c1_rounds_match_independent_restatement(pt, flags, ptp):
-    s = pt.Scene.config(1)
-    W, H, schedule = 16, 12, [2, 1, 1]
-    slots, accum = pr.render(s, W, H, schedule, flags=flags, ptp=ptp)
+def check(s, W, H, schedule, flags, ptp=0.0, camera=0):
+    """Render with both and compare everything; returns the oracle accumulator."""
+    pr.STATS.clear()
+    slots, accum = pr.render(s, W, H, schedule, flags=flags, ptp=ptp, camera=camera)
     o = oracle_lib.OracleRenderer(s.packs(), W, H)
     o.RenderFlags = flags
     o.PathTerminationProbability = ptp
+    o.CameraIndex = camera
     o.reset()
     for r in schedule:
         o.run(r)
@@ -47,6 +52,13 @@ def test_c1_rounds_match_independent_restatement(pt, flags, ptp):
             assert (act[1] << 16 | act[0]) == int(want["active01"]), (where, "active01")
             assert (act[3] << 16 | act[2]) == int(want["active23"]), (where, "active23")
     assert np.array_equal(bits(accum), oa.view(np.uint32)), "accumulator"
+    return oa
+
+
+@pytest.mark.parametrize("flags,ptp", [(3, 0.0), (1, 0.0), (3, 0.3), (2, 0.0)])
+def test_c1_rounds_match_independent_restatement(pt, flags, ptp):
+    s = pt.Scene.config(1)
+    oa = check(s, 16, 12, [2, 1, 1], flags, ptp)
     assert oa[..., 3].sum() > 0
     s.close()
 
@@ -55,25 +67,38 @@ def test_c1_rounds_match_independent_restatement(pt, flags, ptp):
 def test_c3_rounds_match_independent_restatement(pt, flags):
     """C3's room: a textured (bilinear) diffuse mesh under a constant sky."""
     s = pt.Scene.config(3)
-    W, H, schedule = 12, 8, [2, 1, 1]
-    slots, accum = pr.render(s, W, H, schedule, flags=flags)
-    o = oracle_lib.OracleRenderer(s.packs(), W, H)
-    o.RenderFlags = flags
-    o.reset()
-    for r in schedule:
-        o.run(r)
-    st, oa = o.state(), o.accum()
-    o.close()
-    for y in range(H):
-        for x in range(W):
-            sl, want = slots[y][x], st[y, x]
-            assert sl.PV == int(want["packed_velocity"]), ((x, y), "velocity")
-            assert np.array_equal(bits(sl.thr), want["throughput"].view(np.uint32)), ((x, y), "throughput")
-            assert np.array_equal(bits(sl.prob), want["probability"].view(np.uint32)), ((x, y), "probability")
-            assert np.array_equal(bits(sl.O), want["origin"].view(np.uint32)), ((x, y), "origin")
-    assert np.array_equal(bits(accum), oa.view(np.uint32)), "accumulator"
+    oa = check(s, 12, 8, [2, 1, 1], flags)
     assert oa[..., 3].sum() > 0 and oa[..., :3].sum() > 0     # escapes reached the sky
     s.close()
+
+
+def test_c2_rounds_match_independent_restatement(pt):
+    """C2: a smooth glass sphere, metal and diffuse shapes, the HDR sky."""
+    s = pt.Scene.config(2)
+    check(s, 16, 12, [2, 1, 1], 3)
+    for branch in ("diffuse", "metal", "glass_dirac", "refract", "light"):
+        assert pr.STATS[branch] > 5, dict(pr.STATS)
+    s.close()
+
+
+def test_fuzz_rounds_match_independent_restatement(pt):
+    """Every fuzz seed of 0-23 without an OpenPBR surface, with its own
+    flags, roulette and camera; together they take every branch."""
+    seen, ran = collections.Counter(), 0
+    for seed in range(24):
+        s, st = fuzz_scenes.build(pt, seed)
+        mats = s.arrays()["materials"].astype(np.uint32)
+        if any(mats[32 * int(m)] == 3 for m in s.arrays()["shapes"]["MaterialIndex"]):
+            s.close()
+            continue
+        check(s, 12, 8, [2, 1, 1], st["flags"], st["termination"], st["camera"])
+        seen.update(pr.STATS)
+        ran += 1
+        s.close()
+    assert ran >= 15
+    for branch in ("diffuse", "metal", "metal_dirac", "glass", "glass_dirac", "reflect", "refract",
+                   "medium", "light"):
+        assert seen[branch] > 20, dict(seen)
 
 
 def metal_room(pt):
@@ -122,28 +147,48 @@ def test_metal_room_rounds_match_independent_restatement(pt, flags, ptp):
     """Metal BSDF sampling and evaluation (GGX, F82-tint Fresnel), sky light
     sampling (vMF) and the textured sky, restated apart from the oracle."""
     s = metal_room(pt)
-    W, H, schedule = 16, 12, [2, 1, 1]
-    pr.STATS.clear()
-    slots, accum = pr.render(s, W, H, schedule, flags=flags, ptp=ptp)
-    o = oracle_lib.OracleRenderer(s.packs(), W, H)
-    o.RenderFlags = flags
-    o.PathTerminationProbability = ptp
-    o.reset()
-    for r in schedule:
-        o.run(r)
-    st, oa = o.state(), o.accum()
-    o.close()
-    for y in range(H):
-        for x in range(W):
-            sl, want = slots[y][x], st[y, x]
-            where = (x, y)
-            assert np.array_equal(bits(sl.O), want["origin"].view(np.uint32)), (where, "origin")
-            assert sl.PV == int(want["packed_velocity"]), (where, "velocity")
-            assert np.array_equal(bits(sl.thr), want["throughput"].view(np.uint32)), (where, "throughput")
-            assert np.array_equal(bits(sl.prob), want["probability"].view(np.uint32)), (where, "probability")
-            assert np.array_equal(bits(sl.sample), want["sample"].view(np.uint32)), (where, "sample")
-    assert np.array_equal(bits(accum), oa.view(np.uint32)), "accumulator"
+    oa = check(s, 16, 12, [2, 1, 1], flags, ptp)
     assert oa[..., 3].sum() > 0 and oa[..., :3].sum() > 0
-    for branch in ("diffuse", "metal", "dirac", "light"):
+    for branch in ("diffuse", "metal", "metal_dirac", "light"):
         assert pr.STATS[branch] > 5, dict(pr.STATS)
+    s.close()
+
+
+def fog_glass(pt):
+    """Scattering glass: a rough glass block holding forward-scattering fog
+    (Henyey-Greenstein g = 0.6) with a smooth, strongly dispersive sphere of
+    back-scattering fog (g = -0.5) nested in it, in a hazy scene medium."""
+    import fuzz_scenes
+    rng = np.random.default_rng(11)
+    s = pt.Scene.empty()
+    floor = s.create_material(pt.MATERIAL_BASIC_DIFFUSE, "Floor", BaseColor=(0.7, 0.7, 0.7))
+    block = s.create_material(pt.MATERIAL_BASIC_TRANSLUCENT, "Block", IOR=1.45, AbbeNumber=40.0, Roughness=0.2,
+                              TransmissionColor=(0.9, 0.8, 0.7), TransmissionDepth=0.6)
+    s.set_material_parameter(block, "ScatteringColor", (0.8, 0.8, 0.9))
+    s.set_material_parameter(block, "ScatteringAnisotropy", 0.6)
+    ball = s.create_material(pt.MATERIAL_BASIC_TRANSLUCENT, "Ball", IOR=1.8, AbbeNumber=20.0, Roughness=0.0,
+                             TransmissionColor=(0.6, 0.9, 0.8), TransmissionDepth=0.4)
+    s.set_material_parameter(ball, "ScatteringColor", (0.5, 0.7, 0.6))
+    s.set_material_parameter(ball, "ScatteringAnisotropy", -0.5)
+    s.create_entity(pt.ENTITY_PLANE, position=(0.0, 0.0, -1.0), material=floor)
+    cube = s.create_entity(pt.ENTITY_CUBE, position=(0.0, 0.0, 0.0), rotation=(0.1, 0.2, 0.3),
+                           scale=(1.4, 1.4, 1.0), material=block)
+    s.create_entity(pt.ENTITY_SPHERE, parent=cube, scale=(0.55, 0.55, 0.7), material=ball)
+    sky = s.create_texture("Sky", pt.TEXTURE_RADIANCE, fuzz_scenes.random_sky(rng))
+    s.set_root(scatter_rate=0.02, skybox_brightness=1.0, skybox_sampling_probability=0.5, skybox=sky)
+    cam = s.create_entity(pt.ENTITY_CAMERA, position=(0.0, -4.5, 0.6), rotation=(1.45, 0.0, 0.0))
+    s.set_camera_pinhole(cam, fov_degrees=50.0)
+    s.pack()
+    return s
+
+
+@pytest.mark.parametrize("flags,ptp", [(3, 0.0), (1, 0.1)])
+def test_fog_glass_rounds_match_independent_restatement(pt, flags, ptp):
+    """Anisotropic medium scattering (SampleDirectionHG), rough refraction
+    and reflection with dispersion, nested media, sky light sampling on
+    rough glass."""
+    s = fog_glass(pt)
+    check(s, 16, 12, [2, 1, 1, 1], flags, ptp)
+    for branch in ("glass", "glass_dirac", "reflect", "refract", "medium_hg", "light"):
+        assert pr.STATS[branch] > 5, sorted(pr.STATS.items())
     s.close()

@@ -28,6 +28,7 @@ from __future__ import annotations
 import numpy as np
 
 import kat
+import oracle_lib
 
 f32 = np.float32
 INFINITY = f32(1e30)             # common.glsl.inc:4
@@ -316,8 +317,8 @@ def _sign(x):
 
 
 def hit_attributes(S, h):
-    """(Normal, TangentX, UV or None) of a hit; UV is None for spheres (their
-    atan2 is a convention function of the numerics layer, not restated)."""
+    """(Normal, TangentX, UV) of a hit (scene.glsl.inc:540-600); a sphere's
+    atan2 is the numerics convention's own (the oracle's exported pt_atan2)."""
     to, frm = S.shape_to[h.shape], S.shape_from[h.shape]
     c = h.coords
     if h.kind == MESH:
@@ -336,7 +337,8 @@ def hit_attributes(S, h):
     elif h.kind == SPHERE:
         normal = _transform_normal(c, frm)
         tangent = _transform_direction(_cross(c, [-c[1], c[0], f32(0.0)]), to)
-        uv = None
+        at = f32(oracle_lib.lib().oracle_fp_atan2(float(c[1]), float(c[0])))
+        uv = [(at + f32(3.141592653)) / f32(6.283185306), (c[2] + f32(1.0)) / f32(2.0)]
     else:
         q = [abs(c[0]), abs(c[1]), abs(c[2])]
         half, one = f32(0.5), f32(1.0)
@@ -356,8 +358,7 @@ def hit_attributes(S, h):
 
 def trace_records(arrays, origins, velocities, durations):
     """Per ray, as StoreTraceHit (basic.glsl.inc:142-156) writes them: time,
-    ShapeAndMaterialIndex, packed normal, packed tangent, U, V (U, V NaN where
-    not restated: sphere hits)."""
+    ShapeAndMaterialIndex, packed normal, packed tangent, U, V (NaN on a miss)."""
     S = Scene(arrays)
     n = len(origins)
     times = np.zeros(n, np.float32)
@@ -375,6 +376,5 @@ def trace_records(arrays, origins, velocities, durations):
         normal, tangent, u = hit_attributes(S, h)
         pn[i] = kat.pack_unit_vector(np.array([normal], np.float32))[0]
         ptg[i] = kat.pack_unit_vector(np.array([tangent], np.float32))[0]
-        if u is not None:
-            uv[i] = u
+        uv[i] = u
     return times, sm, pn, ptg, uv
