@@ -4,7 +4,7 @@ tests/trace_restatement.py for Trace): after Reset, Run(2), Run(1), Run(1),
 every slot's ray, Lambda0, throughput, probability, sample and active-shape
 words, and every accumulated pixel, bit for bit -- on C1 (diffuse sphere and
 plane, nearest checker, constant sky), C2 (glass, metal, HDR sky sampled by
-the vMF lobe), C3 (the room mesh, bilinear texture), a metal room, and the
+the vMF lobe), C5 (both cameras), C3 (the room mesh, bilinear texture), a metal room, and the
 random fuzz scenes without OpenPBR (rough and smooth glass with dispersion,
 nested and scattering media, a scattering scene medium, textured roughness,
 every camera model); with and without jitter, with Russian roulette,
@@ -72,11 +72,17 @@ def test_c3_rounds_match_independent_restatement(pt, flags):
     s.close()
 
 
-def test_c2_rounds_match_independent_restatement(pt):
-    """C2: a smooth glass sphere, metal and diffuse shapes, the HDR sky."""
-    s = pt.Scene.config(2)
-    check(s, 16, 12, [2, 1, 1], 3)
-    for branch in ("diffuse", "metal", "glass_dirac", "refract", "light"):
+@pytest.mark.parametrize("config,camera,branches", [
+    (2, 0, ("diffuse", "metal", "glass_dirac", "refract", "light")),
+    (5, 0, ("diffuse", "metal", "glass_dirac", "refract")),
+    (5, 1, ("diffuse", "metal", "refract"))])
+def test_config_rounds_match_independent_restatement(pt, config, camera, branches):
+    """C2 (a smooth glass sphere, metal and diffuse shapes, the HDR sky) and
+    C5 (every basic material, a scattering medium, both of its cameras)."""
+    s = pt.Scene.config(config)
+    info = s.info
+    check(s, 16, 12, [2, 1, 1], info.render_flags, info.termination_probability, camera)
+    for branch in branches:
         assert pr.STATS[branch] > 5, dict(pr.STATS)
     s.close()
 
