@@ -25,10 +25,11 @@ Reset / Run(k) leave in the slot state and the accumulator:
   CauchyEmpiricalIOR, ComputeCosThetaRefracted, FresnelDielectric  common.glsl.inc:356-420
   SampleDirectionHG (medium scattering in Scatter)         common.glsl.inc:256-276
 
-Scope: the three basic materials (no OpenPBR surface), nested media with
+Scope: the three basic materials and OpenPBR's default fall-through (the
+reference's dispatch has no OpenPBR case, so such a hit ends the path), nested media with
 absorption and scattering, a scattering scene medium; the sky may be
-textured and light-sampled (C1, C2, C3, a metal room, the fuzz scenes
-without OpenPBR).
+textured and light-sampled (C1-C5, a metal room, a scattering-glass scene,
+the fuzz scenes).  Not covered: the opt-in OpenPBR sampler.
 Numerics: DESIGN.md §2's convention (float32, nothing fused, reductions left
 to right, normalize = v * (1 / sqrt(dot)), mix = x*(1-a) + y*a); exp, log,
 sin, cos, atan2, asin are the convention's own functions (the oracle's
@@ -303,7 +304,7 @@ class World:
         self.atlas = np.frombuffer((C.c_float * n).from_address(packs.atlas), np.float32).reshape(
             layers, self.ah, self.aw, 4) if n else None
         for m in self.S.shape_material:
-            assert self.mat[32 * m] in (0, 1, 2), "scope: the basic materials only"
+            assert self.mat[32 * m] in (0, 1, 2, 3), "scope: material types 0-3"
 
     def mfloat(self, m, a):
         return self.mat[32 * m + a:32 * m + a + 1].view(np.float32)[0]
@@ -446,6 +447,8 @@ def evaluate_bsdf(W_, m, lam, uv, exterior, In, Out):
     (ok, throughput, probability)."""
     if W_.mat[32 * m] == 2:
         return translucent_evaluate(W_, m, lam, uv, exterior, In, Out)
+    if W_.mat[32 * m] == 3:   # OpenPBR: not dispatched (scene.glsl.inc:686-692,735)
+        return False, None, None
     if W_.mat[32 * m] == 0:
         r = W_.reflectance(m, lam, uv)
         p = In[2] / PI
@@ -466,6 +469,8 @@ def sample_bsdf(W_, g, m, lam, uv, exterior, In):
     """MaterialSampleBSDF: (ok, Out, throughput, probability)."""
     if W_.mat[32 * m] == 2:
         return translucent_sample(W_, g, m, lam, uv, exterior, In)
+    if W_.mat[32 * m] == 3:
+        return False, None, None, None
     if W_.mat[32 * m] == 0:
         d = random_direction(g)
         Out = _safe_normalize([d[0], d[1], d[2] + f32(1.0)])
@@ -583,7 +588,7 @@ def sample_surface_integrand(W_, g, m, lam, uv, exterior, TX, TY, N, out):
     dirac = (typ == 1 and W_.value(m, 9, uv) < f32(1e-3)) or (typ == 2 and W_.value(m, 3, uv) < f32(1e-3))
     light_p = f32(0.0) if dirac else W_.light_p
     mu = [_dot(W_.sky_mean, TX), _dot(W_.sky_mean, TY), _dot(W_.sky_mean, N)]
-    STATS[("diffuse", "metal", "glass")[typ] + ("_dirac" if dirac else "")] += 1
+    STATS[("diffuse", "metal", "glass", "openpbr")[typ] + ("_dirac" if dirac else "")] += 1
     if g.r01() < light_p:
         STATS["light"] += 1
         inn = random_vmf(g, W_.kappa, mu)
