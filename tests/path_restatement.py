@@ -25,11 +25,13 @@ Reset / Run(k) leave in the slot state and the accumulator:
   CauchyEmpiricalIOR, ComputeCosThetaRefracted, FresnelDielectric  common.glsl.inc:356-420
   SampleDirectionHG (medium scattering in Scatter)         common.glsl.inc:256-276
 
-Scope: the three basic materials and OpenPBR's default fall-through (the
-reference's dispatch has no OpenPBR case, so such a hit ends the path), nested media with
+Scope: the three basic materials, OpenPBR's default fall-through (the
+reference's dispatch has no OpenPBR case, so such a hit ends the path) and
+the opt-in OpenPBR sampler (openpbr.glsl.inc:66-515 with DESIGN.md §6 row
+4's deviations (a)-(d)), nested media with
 absorption and scattering, a scattering scene medium; the sky may be
 textured and light-sampled (C1-C5, a metal room, a scattering-glass scene,
-the fuzz scenes).  Not covered: the opt-in OpenPBR sampler.
+the fuzz scenes, tests/test_openpbr.py's scene).
 Numerics: DESIGN.md §2's convention (float32, nothing fused, reductions left
 to right, normalize = v * (1 / sqrt(dot)), mix = x*(1-a) + y*a); exp, log,
 sin, cos, atan2, asin are the convention's own functions (the oracle's
@@ -293,6 +295,7 @@ class World:
         self.mat = self.arrays["materials"].astype(np.uint32)
         self.tex = self.arrays["textures"]
         g = self.arrays["globals"][0]
+        self.openpbr = False   # ptSetBasicRendererOpenPBR (the opt-in OpenPBR sampler)
         self.sky_index = int(g["SkyboxTextureIndex"])
         self.light_p = f32(g["SkyboxSamplingProbability"])
         self.sky_brightness = f32(g["SkyboxBrightness"])
@@ -422,15 +425,20 @@ def resolve_medium(W_, shape, lam):
     if shape == NONE:
         return NONE, [f32(1.0)] * 4, zero, [W_.scatter_rate] * 4, f32(0.0)
     m = W_.S.shape_material[shape]
-    if W_.mat[32 * m] != 2:
+    typ = W_.mat[32 * m]
+    if typ == 2:     # BasicTranslucent_LoadMedium
+        a_ior, a_abbe, a_depth, a_tr, a_sc, a_aniso = 1, 2, 10, 7, 11, 14
+    elif typ == 3 and W_.openpbr:   # OpenPBR_Medium (openpbr.glsl.inc:160-191)
+        a_ior, a_abbe, a_depth, a_tr, a_sc, a_aniso = 13, 26, 25, 17, 21, 24
+    else:
         return shape, [f32(1.0)] * 4, zero, zero, f32(0.0)
-    ior = cauchy_ior(W_.mfloat(m, 1), W_.mfloat(m, 2), lam)
-    depth = W_.mfloat(m, 10)
+    ior = cauchy_ior(W_.mfloat(m, a_ior), W_.mfloat(m, a_abbe), lam)
+    depth = W_.mfloat(m, a_depth)
     if depth > 0:
-        tr_ = [parametric([W_.mfloat(m, 7), W_.mfloat(m, 8), W_.mfloat(m, 9)], l) for l in lam]
-        sc = [parametric([W_.mfloat(m, 11), W_.mfloat(m, 12), W_.mfloat(m, 13)], l) / depth for l in lam]
+        tr_ = [parametric([W_.mfloat(m, a_tr + i) for i in range(3)], l) for l in lam]
+        sc = [parametric([W_.mfloat(m, a_sc + i) for i in range(3)], l) / depth for l in lam]
         ext = [-_fp("log", t) / depth for t in tr_]
-        return shape, ior, [np.fmax(ext[k] - sc[k], f32(0.0)) for k in range(4)], sc, W_.mfloat(m, 14)
+        return shape, ior, [np.fmax(ext[k] - sc[k], f32(0.0)) for k in range(4)], sc, W_.mfloat(m, a_aniso)
     return shape, ior, zero, zero, f32(0.0)
 
 
@@ -470,7 +478,10 @@ def sample_bsdf(W_, g, m, lam, uv, exterior, In):
     if W_.mat[32 * m] == 2:
         return translucent_sample(W_, g, m, lam, uv, exterior, In)
     if W_.mat[32 * m] == 3:
-        return False, None, None, None
+        if not W_.openpbr:
+            return False, None, None, None
+        q = openpbr_parameters(W_, g, m, lam, uv, exterior)
+        return openpbr_sample(g, q, In)
     if W_.mat[32 * m] == 0:
         d = random_direction(g)
         Out = _safe_normalize([d[0], d[1], d[2] + f32(1.0)])
@@ -582,10 +593,196 @@ def translucent_sample(W_, g, m, lam, uv, exterior, In):
     return True, Out, [p[k] * gs for k in range(4)], p
 
 
+def _pow(x, y):
+    """pow(x, y) = exp(y log x) on the convention's exp / log."""
+    return _fp("exp", y * _fp("log", x))
+
+
+class OpenPBRParameters:
+    pass
+
+
+def openpbr_parameters(W_, g, m, lam, uv, exterior):
+    """OpenPBR_Parameters (openpbr.glsl.inc:66-158); Emission is never read
+    by OpenPBR_Sample and is not evaluated."""
+    f = lambda a: W_.mfloat(m, a)   # noqa: E731
+    q = OpenPBRParameters()
+    q.lam = lam
+    q.coat = g.r01() < f(32)
+    q.metal = g.r01() < f(7)
+    q.translucent = (not q.metal) and g.r01() < f(20)
+    q.base = [f(2) * parametric([f(3), f(4), f(5)], l) for l in lam]
+    q.diffuse_roughness = f(8)
+    ti = int(W_.mat[32 * m + 6])
+    if ti != NONE:
+        tb = W_.sample_texture(ti, uv)
+        q.base = [q.base[k] * parametric([tb[0], tb[1], tb[2]], lam[k]) for k in range(4)]
+    if q.coat:
+        q.coat_rel = [exterior[k] / f(36) for k in range(4)]
+        q.coat_tr = [parametric([f(33), f(34), f(35)], l) for l in lam]
+        q.coat_alpha = ggx_alpha(f(37), f(38))
+    q.spec_weight = f(9)
+    q.spec = [parametric([f(10), f(11), f(12)], l) for l in lam]
+    sior = cauchy_ior(f(13), f(26), lam)
+    if q.coat:
+        q.spec_rel = [f(36) / sior[k] for k in range(4)]
+    else:
+        q.spec_rel = [exterior[k] / sior[k] for k in range(4)]
+    rough = f(14)
+    ti = int(W_.mat[32 * m + 15])
+    if ti != NONE:
+        rough = rough * W_.sample_texture(ti, uv)[0]
+    q.spec_alpha = ggx_alpha(rough, f(16))
+    q.bounces = int(W_.mat[32 * m + 1])
+    return q
+
+
+def _sgn3(v):
+    s_ = np.sign(v[2])
+    return [v[0] * s_, v[1] * s_, v[2] * s_]
+
+
+def openpbr_coat(g, q, Out, thr, dens):
+    """OpenPBR_CoatSample (openpbr.glsl.inc:194-283); the Fresnel call takes
+    (Eta, CosTheta, CosThetaRefracted)."""
+    if not q.coat:
+        return [-Out[0], -Out[1], -Out[2]], thr, dens
+    u1 = g.r01()
+    u2 = g.r01()
+    n = ggx_visible_normal(_sgn3(Out), q.coat_alpha, u1, u2)
+    c = _dot(n, Out)
+    rel = q.coat_rel
+    if Out[2] < 0:
+        rel = [f32(1.0) / r for r in rel]
+    one = f32(1.0)
+    rcs = one - (rel[0] * rel[0]) * (one - c * c)
+    rc = -np.sign(Out[2]) * np.sqrt(np.fmax(rcs, f32(0.0)))
+    refl = fresnel_dielectric(rel[0], c, rc)
+    if g.r01() < refl:
+        STATS["coat_reflect"] += 1
+        In = [(f32(2.0) * c) * n[i] - Out[i] for i in range(3)]
+        if In[2] * Out[2] <= 0:
+            return In, thr, [f32(0.0)] * 4
+        g1 = ggx_g1(In, q.coat_alpha)
+        thr = [t * g1 for t in thr]
+        if Out[2] < 0:
+            e = -(f32(0.5) / Out[2] + f32(0.5) / In[2])
+            thr = [thr[k] * _pow(q.coat_tr[k], e) for k in range(4)]
+    else:
+        STATS["coat_refract"] += 1
+        In = [(rel[0] * c + rc) * n[i] - rel[0] * Out[i] for i in range(3)]
+        if In[2] * Out[2] > 0:
+            return In, thr, [f32(0.0)] * 4
+        g1 = ggx_g1(In, q.coat_alpha)
+        thr = [t * g1 for t in thr]
+        e = f32(-0.5) / Out[2] if Out[2] < 0 else f32(-0.5) / In[2]
+        thr = [thr[k] * _pow(q.coat_tr[k], e) for k in range(4)]
+    return In, thr, dens
+
+
+def openpbr_specular(g, q, Out, thr, dens):
+    """OpenPBR_BaseSpecularSample (openpbr.glsl.inc:286-435); rough
+    refraction keeps the reference's zero Fresnel vector (:390-391)."""
+    one = f32(1.0)
+    u1 = g.r01()
+    u2 = g.r01()
+    n = ggx_visible_normal(_sgn3(Out), q.spec_alpha, u1, u2)
+    c = _dot(n, Out)
+    if q.metal:
+        STATS["spec_metal"] += 1
+        In = [(f32(2.0) * c) * n[i] - Out[i] for i in range(3)]
+        if Out[2] * In[2] <= 0:
+            return In, thr, [f32(0.0)] * 4
+        sh = ggx_g1(Out, q.spec_alpha)
+        fr = [q.spec_weight * x for x in schlick_fresnel_metal(q.base, q.spec, abs(c))]
+        return In, [thr[k] * (fr[k] * sh) for k in range(4)], dens
+    rel = q.spec_rel
+    if Out[2] < 0:
+        rel = [one / r for r in rel]
+    if q.spec_weight < one:
+        sw = np.sqrt(q.spec_weight)
+        R = [(sw * (one - r)) / (one + r) for r in rel]
+        rel = [(one - x) / (one + x) for x in R]
+    rc = cos_refracted(rel[0], c)
+    refl = fresnel_dielectric(rel[0], c, rc)
+    if g.r01() < refl:
+        STATS["spec_reflect"] += 1
+        In = [(f32(2.0) * c) * n[i] - Out[i] for i in range(3)]
+        if In[2] * Out[2] <= 0:
+            return In, thr, [f32(0.0)] * 4
+        if Out[2] > 0:
+            thr = [thr[k] * q.spec[k] for k in range(4)]
+        g1 = ggx_g1(In, q.spec_alpha)
+        return In, [t * g1 for t in thr], dens
+    In = [(rel[0] * c + rc) * n[i] - rel[0] * Out[i] for i in range(3)]
+    if In[2] * Out[2] > 0:
+        return In, thr, [f32(0.0)] * 4
+    sh = ggx_g1(In, q.spec_alpha)
+    a = q.spec_alpha
+    STATS["spec_refract"] += 1
+    if np.sqrt(a[0] * a[0] + a[1] * a[1]) > EPSILON:
+        fr = [f32(0.0)] * 4
+        ns = [None] + [_safe_normalize([In[i] + Out[i] * rel[k] for i in range(3)]) for k in (1, 2, 3)]
+        d = [ggx_distribution(n, a), f32(0.0), f32(0.0), f32(0.0)]
+        for k in (1, 2, 3):
+            if _dot(In, ns[k]) * _dot(Out, ns[k]) < 0:
+                d[k] = ggx_distribution(ns[k], a)
+        mx = np.fmax(EPSILON, _max4(d))
+        d = [x / mx for x in d]
+        return In, [thr[k] * ((d[k] * fr[k]) * sh) for k in range(4)], [dens[k] * (d[k] * fr[k]) for k in range(4)]
+    return (In, [thr[0] * sh, thr[1] * f32(0.0), thr[2] * f32(0.0), thr[3] * f32(0.0)],
+            [dens[0] * one, dens[1] * f32(0.0), dens[2] * f32(0.0), dens[3] * f32(0.0)])
+
+
+def openpbr_diffuse(g, q, Out, thr):
+    """OpenPBR_BaseDiffuseSample (openpbr.glsl.inc:438-461): Oren-Nayar."""
+    if q.translucent:
+        return [-Out[0], -Out[1], -Out[2]], thr
+    STATS["oren_nayar"] += 1
+    d = random_direction(g)
+    In = _safe_normalize([d[0], d[1], d[2] + f32(1.0)])
+    S = _dot(In, Out) - In[2] * Out[2]
+    T = np.fmax(In[2], Out[2]) if S > 0 else f32(1.0)
+    s2 = q.diffuse_roughness * q.diffuse_roughness
+    one = f32(1.0)
+    A = [(one - (f32(0.5) * s2) / (s2 + f32(0.33))) + ((f32(0.17) * b) * s2) / (s2 + f32(0.13)) for b in q.base]
+    B = (f32(0.45) * s2) / (s2 + f32(0.09))
+    return In, [thr[k] * (q.base[k] * (A[k] + (B * S) / T)) for k in range(4)]
+
+
+def openpbr_sample(g, q, Out):
+    """OpenPBR_Sample (openpbr.glsl.inc:463-515): the layer walk.
+    (ok, In, throughput, probability); In = -Out with no bounce (DESIGN.md
+    §6 row 4 (c))."""
+    EXTERNAL, COAT, SPEC, DIFF = -1, 0, 1, 2
+    STATS["openpbr_walk"] += 1
+    layer = (COAT if q.coat else SPEC) if Out[2] > 0 else SPEC
+    thr = [f32(1.0)] * 4
+    dens = [f32(1.0)] * 4
+    In = [-Out[0], -Out[1], -Out[2]]
+    for _ in range(q.bounces):
+        if layer == COAT:
+            In, thr, dens = openpbr_coat(g, q, Out, thr, dens)
+            layer = SPEC if In[2] < 0 else EXTERNAL
+        elif layer == SPEC:
+            In, thr, dens = openpbr_specular(g, q, Out, thr, dens)
+            layer = DIFF if In[2] < 0 else COAT
+        elif layer == DIFF:
+            In, thr = openpbr_diffuse(g, q, Out, thr)
+            layer = EXTERNAL if In[2] < 0 else SPEC
+        else:
+            break
+        if _max4(dens) < EPSILON:
+            return False, None, None, None
+        Out = [-In[0], -In[1], -In[2]]
+    return True, In, thr, dens
+
+
 def sample_surface_integrand(W_, g, m, lam, uv, exterior, TX, TY, N, out):
     """SampleSurfaceIntegrand (basic_scatter.glsl:68-109): (ok, In, throughput, probability)."""
     typ = int(W_.mat[32 * m])
-    dirac = (typ == 1 and W_.value(m, 9, uv) < f32(1e-3)) or (typ == 2 and W_.value(m, 3, uv) < f32(1e-3))
+    dirac = ((typ == 1 and W_.value(m, 9, uv) < f32(1e-3)) or (typ == 2 and W_.value(m, 3, uv) < f32(1e-3))
+             or (typ == 3 and W_.openpbr))   # the OpenPBR sampler has no evaluate: never light-sampled
     light_p = f32(0.0) if dirac else W_.light_p
     mu = [_dot(W_.sky_mean, TX), _dot(W_.sky_mean, TY), _dot(W_.sky_mean, N)]
     STATS[("diffuse", "metal", "glass", "openpbr")[typ] + ("_dirac" if dirac else "")] += 1
@@ -702,9 +899,10 @@ def store_active(sl):
     sl.active = out
 
 
-def render(scene, W, H, schedule, flags=3, ptp=0.0, camera=0):
+def render(scene, W, H, schedule, flags=3, ptp=0.0, camera=0, openpbr=False):
     """Reset + Run(r) for r in schedule (FrameIndex from 0): (slots, accum)."""
     W_ = World(scene)
+    W_.openpbr = openpbr
     cam = W_.arrays["cameras"][camera]
     ptp = f32(ptp)
     accum = np.zeros((H, W, 4), np.float32)

@@ -25,11 +25,12 @@ def bits(a):
     return np.asarray(a, np.float32).view(np.uint32)
 
 
-def check(s, W, H, schedule, flags, ptp=0.0, camera=0):
+def check(s, W, H, schedule, flags, ptp=0.0, camera=0, openpbr=False):
     """Render with both and compare everything; returns the oracle accumulator."""
     pr.STATS.clear()
-    slots, accum = pr.render(s, W, H, schedule, flags=flags, ptp=ptp, camera=camera)
+    slots, accum = pr.render(s, W, H, schedule, flags=flags, ptp=ptp, camera=camera, openpbr=openpbr)
     o = oracle_lib.OracleRenderer(s.packs(), W, H)
+    o.set_openpbr(openpbr)
     o.RenderFlags = flags
     o.PathTerminationProbability = ptp
     o.CameraIndex = camera
@@ -192,4 +193,19 @@ def test_fog_glass_rounds_match_independent_restatement(pt, flags, ptp):
     check(s, 16, 12, [2, 1, 1, 1], flags, ptp)
     for branch in ("glass", "glass_dirac", "reflect", "refract", "medium_hg", "light"):
         assert pr.STATS[branch] > 5, sorted(pr.STATS.items())
+    s.close()
+
+
+@pytest.mark.parametrize("flags,ptp", [(3, 0.0), (2, 0.1)])
+def test_openpbr_sampler_rounds_match_independent_restatement(pt, flags, ptp):
+    """The opt-in OpenPBR sampler (ptSetBasicRendererOpenPBR) on
+    tests/test_openpbr.py's scene: parameter draws, coat, metal and
+    dielectric base specular, Oren-Nayar diffuse base, the layer walk with a
+    bounce limit of 3, OpenPBR media nested with a basic glass."""
+    import test_openpbr
+    s = test_openpbr.openpbr_scene(pt)
+    check(s, 16, 12, [2, 1, 1, 1], flags, ptp, openpbr=True)
+    for branch in ("coat_reflect", "coat_refract", "spec_metal", "spec_reflect", "spec_refract", "oren_nayar",
+                   "medium_hg", "light"):
+        assert pr.STATS[branch] > 10, sorted(pr.STATS.items())
     s.close()
