@@ -87,9 +87,11 @@ def intersect_bounding_box(O, V, reach, mn, mx):
 
 
 class Hit:
-    __slots__ = ("time", "shape", "prim", "kind", "coords")
+    __slots__ = ("time", "shape", "prim", "kind", "coords", "scene_complexity", "mesh_complexity")
 
     def __init__(self, duration):
+        self.scene_complexity = 0   # shape nodes visited (scene.glsl.inc:117, 480)
+        self.mesh_complexity = 0    # mesh nodes visited (:118, 345)
         self.time = f32(duration)
         self.shape = SHAPE_INDEX_NONE
         self.prim = 0
@@ -162,6 +164,7 @@ def intersect_mesh_node(S, O, V, root, hit):
     stack = []
     node = root
     while True:
+        hit.mesh_complexity += 1
         if S.mn_end[node] > 0:
             for face in range(S.mn_begin[node], S.mn_end[node]):
                 intersect_mesh_face(S, O, V, face, hit)
@@ -246,6 +249,7 @@ def trace(S, O, V, duration):
     stack = []
     node = 0
     while True:
+        hit.scene_complexity += 1
         children = S.sn_children[node]
         if children == 0:
             intersect_shape(S, O, V, S.sn_shape[node], hit)
