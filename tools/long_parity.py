@@ -7,7 +7,7 @@ pixel compared with the CPU oracle bit for bit.  Prints one JSON line.
 A random scene of tests/fuzz_scenes.py runs as CONFIG "fuzz:SEED" at
 320x240 with the seed's RenderFlags, roulette and camera.
 
-usage: python tools/long_parity.py [CONFIG | fuzz:SEED] [ROUNDS]"""
+usage: python tools/long_parity.py [CONFIG | fuzz:SEED] [ROUNDS] [CAMERA]"""
 import json
 import sys
 import time
@@ -35,6 +35,8 @@ def main():
         s = pt.Scene.config(cfg)
         info = s.info
         W, H, flags, ptp, camera = info.width, info.height, info.render_flags, info.termination_probability, 0
+        if len(sys.argv) > 3:
+            camera = int(sys.argv[3])
     dev = pt.Device(0)
     ds = pt.DeviceScene(dev)
     ds.update(s)
@@ -59,7 +61,7 @@ def main():
     for f in ("origin", "packed_velocity", "lambda0", "throughput", "probability", "sample", "active01", "active23"):
         bad[f] = int(np.sum(np.any((g[f].view(np.uint32) != want[f].view(np.uint32)).reshape(H, W, -1), axis=-1)))
     acc_bad = int(np.sum(np.any(sb.read().view(np.uint32) != o.accum().view(np.uint32), axis=-1)))
-    print(json.dumps({"config": cfg, "size": [W, H], "rounds": rounds, "state_mismatch_px": bad,
+    print(json.dumps({"config": cfg, "camera": camera, "size": [W, H], "rounds": rounds, "state_mismatch_px": bad,
                       "accum_mismatch_px": acc_bad, "samples": float(o.accum()[..., 3].sum()),
                       "seconds": round(time.time() - t0, 1)}), flush=True)
 
