@@ -52,7 +52,9 @@ HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # records, independent of this build's layout): extend reads the 20-B ray and
 # writes the 24-B hit; shade reads path 60 + ray/hit 44 and writes ray 20 +
 # path vertex 52.  Sum = the 220 B/ray whole-path figure.
-ALG_BYTES = {"extend": 44, "shade": 176, "round": 220}   # round: fused extend + shade (small partitions)
+# round: fused extend + shade (small partitions); rounds: a round batch (per round it covers)
+ALG_BYTES = {"extend": 44, "shade": 176, "round": 220, "rounds": 220}
+KERNEL_IDS = {"extend": 1, "shade": 2, "round": 5, "rounds": 6}   # pt_api.h PT_KERNEL_*
 L2_PEAK_GBPS = 34500.0   # aggregate L2 bandwidth (MI355X_MICROARCH.md § L2)
 PATH_BYTES_PER_RAY = 220  # SURVEY.md §8(d) whole-path definition
 STEADY_ROUNDS = 64        # secondary key: steady-state rounds timed after the frames
@@ -160,6 +162,11 @@ def launch_check(args, world, rank):
     import torch
     import torch.distributed as dist
     dist.init_process_group("gloo")
+    if args.inject_failure == rank:
+        # A rank failing mid-frame (a device fault, an RCCL abort, a bad
+        # argument): it raises here, before the exchange its peers block in;
+        # the launcher then stops the other ranks and the launch exits non-zero.
+        raise RuntimeError(f"bench: injected failure on rank {rank}")
     t = torch.tensor([float(rank + 1)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     acc = torch.ones(4 * 64 * 64, dtype=torch.float32)
@@ -188,6 +195,8 @@ def main():
                     help="every rank on device 0 (multi-rank flow check on a one-GPU box; timings not meaningful)")
     ap.add_argument("--launch-check", action="store_true",
                     help="N-rank launch plumbing only (gloo, no GPU): CPU test of the launcher")
+    ap.add_argument("--inject-failure", type=int, default=-1, metavar="RANK",
+                    help="with --launch-check: this rank raises before the exchange (tests the failure path)")
     ap.add_argument("--shard", choices=("auto", "samples", "bands"), default="auto",
                     help="multi-GPU split: samples (whole frame per rank, own RNG stream) or 16-row pixel bands; "
                          "auto = bands for C4 (pixel-tiled by its config), samples otherwise")
@@ -326,9 +335,9 @@ def main():
     dev.synchronize()
     barrier()
     dt = time.perf_counter() - t0
-    n_ext, ms_ext = dev.kernel_stats(1)
-    n_sh, ms_sh = dev.kernel_stats(2)
-    n_rd, ms_rd = dev.kernel_stats(5)    # fused rounds (a partition that fits the GPU at once)
+    # Per kernel: timed launches, rounds they covered (a round batch covers
+    # several) and their total time.
+    kstats = {k: (*dev.kernel_stats(i), dev.kernel_rounds(i)) for k, i in KERNEL_IDS.items()}
     dev.set_profiling(False)
 
     rounds_local = sum(f[0] for f in frames)
@@ -384,12 +393,14 @@ def main():
         return
 
     mrays = rays / dt / 1e6
-    avg_ext = ms_ext / max(n_ext, 1) if n_ext else ms_rd / max(n_rd, 1)   # traversal-level cache rate below
     kernels = {}
-    for name, n_k, ms_k in (("extend", n_ext, ms_ext), ("shade", n_sh, ms_sh), ("round", n_rd, ms_rd)):
+    for name, (n_k, ms_k, rounds_k) in kstats.items():
         if n_k:
-            avg = ms_k / n_k
-            kernels[name] = {"avg_ms": avg, "gbps": ALG_BYTES[name] * slots_owned / (avg * 1e-3) / 1e9}
+            avg = ms_k / max(rounds_k, 1)   # per round (= per launch except for round batches)
+            kernels[name] = {"avg_ms": avg, "gbps": ALG_BYTES[name] * slots_owned / (avg * 1e-3) / 1e9,
+                             "launches": n_k, "rounds": rounds_k}
+    # traversal-level cache rate below: extend's time per round, or the fused kernels'
+    avg_ext = next(kernels[k]["avg_ms"] for k in ("extend", "round", "rounds") if k in kernels)
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
     achieved = kernels[dom]["gbps"]
     prof = profile_for(args.config) or {}
@@ -458,7 +469,8 @@ def main():
             "alg_bytes_per_launch": ALG_BYTES[dom] * slots_owned,
             "alg_bytes_per_slot": ALG_BYTES[dom],
             "launch_avg_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
-            "launches_timed": {"extend": n_ext, "shade": n_sh, "round": n_rd, "every_nth_round": args.profile_period},
+            "launches_timed": {**{k: v[0] for k, v in kstats.items()}, "every_nth_round": args.profile_period},
+            "rounds_timed": {k: v[2] for k, v in kstats.items()},
             "path_gbps_220B_per_ray": round(PATH_BYTES_PER_RAY * rays / dt / 1e9, 2),
         },
         # What bounds the dominant kernel instead of HBM (PMC of this config's

@@ -97,7 +97,7 @@ enum {
     PT_KERNEL_RESOLVE = 3,
     PT_KERNEL_PREVIEW = 4,
     PT_KERNEL_ROUND   = 5,   /* fused extend + shade of a small partition (one launch per round) */
-    PT_KERNEL_SORT    = 6,   /* global ray sort before extend (scan + scatter) */
+    PT_KERNEL_ROUNDS  = 6,   /* a round batch: several rounds of every tile in one launch */
     PT_KERNEL_COUNT   = 7,
 };
 
@@ -160,6 +160,22 @@ int        ptGetDeviceCount(int* count);
 pt_scene* ptCreateScene(pt_device* device);
 int       ptUpdateScene(pt_device* device, pt_scene* scene, const pt_scene_packs* packs, uint32_t dirty_flags);
 void      ptDestroyScene(pt_device* device, pt_scene* scene);
+/* Encodings chosen per scene at ptUpdateScene (no effect on results; the
+ * wider forms are what larger scenes need, so tests force them on small
+ * ones).  Stack format: AUTO = 16-bit entries when every TLAS / BLAS entry
+ * fits, else packed 32-bit BLAS words when every node fits, else node
+ * indices; WORDS32 / NODE_INDEX force the wider forms.  Hit record: AUTO =
+ * the hit face's vertex indices when they fit 21 bits, else its face index;
+ * FACE_INDEX forces the latter.  Take effect at the next ptUpdateScene. */
+enum {
+    PT_STACK_FORMAT_AUTO       = 0,
+    PT_STACK_FORMAT_WORDS32    = 1,
+    PT_STACK_FORMAT_NODE_INDEX = 2,
+    PT_HIT_RECORD_AUTO         = 0,
+    PT_HIT_RECORD_FACE_INDEX   = 1,
+};
+int       ptSetSceneStackFormat(pt_scene* scene, uint32_t format);
+int       ptSetSceneHitRecordForm(pt_scene* scene, uint32_t form);
 /* Traversal stack entries the uploaded scene can need (TLAS depth + deepest
  * BLAS depth, each capped at the reference's Stack[32]); the extend kernel keeps
  * 20 in LDS and spills the rest to a per-ray global buffer. */
@@ -190,15 +206,11 @@ pt_basic_renderer_params* ptBasicRendererParams(pt_basic_renderer* renderer);
 int                ptResetBasicRenderer(pt_device* device, pt_basic_renderer* renderer);
 int                ptRunBasicRenderer(pt_device* device, pt_basic_renderer* renderer, uint32_t rounds);
 uint32_t           ptBasicRendererSlotCount(pt_basic_renderer* renderer);
-/* Independent tile groups a Run advances on their own streams (1 for a
- * renderer that fills the GPU; more for small partitions);
- * each kernel launch covers one group's tiles. */
-uint32_t           ptBasicRendererRunGroups(pt_basic_renderer* renderer);
 /* Fused rounds: 0 = never (extend then shade launches), 1 = automatic (one
  * extend+shade launch per round when every tile of the renderer fits on the
  * GPU at once: a rank's share of a strongly scaled frame), 2 = whenever the
  * scene allows (no spilled traversal stack).  Results are identical in every
- * mode.  Default 1, or the PT_ROUND_FUSED environment variable. */
+ * mode.  Default 1. */
 int                ptSetBasicRendererFusedRounds(pt_basic_renderer* renderer, int mode);
 /* Consecutive rounds: ptRunBasicRendererRounds(d, r, k) is k calls of
  * ptRunBasicRenderer(d, r, 1) -- the application's frame loop, one new
@@ -209,8 +221,7 @@ int                ptSetBasicRendererFusedRounds(pt_basic_renderer* renderer, in
  * 0 = automatic (16 rounds per launch when every tile of the renderer fits on
  * the GPU at once and fused rounds are automatic, else one round per launch
  * pair), 1 = never, R >= 2 = R whenever the scene allows (no spilled stack).
- * Default 0, or the PT_ROUND_BATCH environment variable.  ptRenderFrame runs
- * its Run(1) rounds this way. */
+ * Default 0.  ptRenderFrame runs its Run(1) rounds this way. */
 int                ptRunBasicRendererRounds(pt_device* device, pt_basic_renderer* renderer, uint32_t count);
 int                ptSetBasicRendererRoundBatch(pt_basic_renderer* renderer, uint32_t rounds);
 /* OpenPBR shading (opt-in extension, no reference counterpart): 0 (default)
@@ -292,12 +303,35 @@ int ptSetProfiling(pt_device* device, int enable);
  * bracketing every launch. */
 int ptSetProfilingPeriod(pt_device* device, uint32_t period);
 int ptGetKernelStats(pt_device* device, int kernel, uint64_t* launches, double* total_ms);
+/* Rounds covered by the timed launches of `kernel` (one per launch, except a
+ * round batch, PT_KERNEL_ROUNDS, which covers its rounds): total_ms / rounds
+ * is the kernel's time per round. */
+int ptGetKernelRounds(pt_device* device, int kernel, uint64_t* rounds);
 int ptResetKernelStats(pt_device* device);
 
-/* RCCL communicator over one process per GPU (xGMI). */
+/* RCCL communicator over one process per GPU (xGMI).
+ *
+ * Failure contract: every ptComm* exchange first agrees
+ * on its argument checks across the ranks (a one-word all-reduce), so a
+ * check that fails on any rank fails the call on every rank and nothing is
+ * exchanged.  While a communicator is live, every call that waits for the
+ * device stream (ptSynchronize, the reads, ptGetStats, ptRenderFrame,
+ * ptUpdateScene, the comm calls' own checks) polls the stream, RCCL's
+ * asynchronous error state and the communicator's deadline instead of
+ * blocking: on an RCCL error it aborts the device's communicators
+ * (ncclCommAbort) and returns PT_ERROR_COMM_ABORTED, at the deadline
+ * PT_ERROR_TIMEOUT.  An aborted communicator fails every later call with
+ * PT_ERROR_COMM_ABORTED; destroy it (and the process normally exits). */
+enum {
+    PT_ERROR_COMM_ABORTED = -2,
+    PT_ERROR_TIMEOUT      = -3,
+};
 int      ptCommGetUniqueId(uint8_t id[128]);
 pt_comm* ptCommCreate(pt_device* device, int nranks, int rank, const uint8_t id[128]);
 void     ptCommDestroy(pt_comm* comm);
+/* Deadline of a wait on the device stream while the communicator is live
+ * (default 600 s: longer than any frame of the benchmark configurations). */
+int      ptCommSetTimeout(pt_comm* comm, double seconds);
 /* Frame-end ncclReduce(sum) of the float4 accumulator to `root` (exact: the
  * ranks' pixel bands are disjoint).  Each rank first zeroes the rows outside
  * the bands of the last partitioned renderer created on the buffer, so the

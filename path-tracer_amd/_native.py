@@ -218,6 +218,8 @@ HIP_API = {
     "ptSynchronize": (_i32, [_vp]),
     "ptCreateScene": (_vp, [_vp]),
     "ptUpdateScene": (_i32, [_vp, _vp, C.POINTER(pt_scene_packs), _u32]),
+    "ptSetSceneStackFormat": (_i32, [_vp, _u32]),
+    "ptSetSceneHitRecordForm": (_i32, [_vp, _u32]),
     "ptDestroyScene": (None, [_vp, _vp]),
     "ptCreateSampleBuffer": (_vp, [_vp, _u32, _u32]),
     "ptDestroySampleBuffer": (None, [_vp, _vp]),
@@ -233,7 +235,6 @@ HIP_API = {
     "ptResetBasicRenderer": (_i32, [_vp, _vp]),
     "ptRunBasicRenderer": (_i32, [_vp, _vp, _u32]),
     "ptBasicRendererSlotCount": (_u32, [_vp]),
-    "ptBasicRendererRunGroups": (_u32, [_vp]),
     "ptSetBasicRendererFusedRounds": (_i32, [_vp, _i32]),
     "ptRunBasicRendererRounds": (_i32, [_vp, _vp, _u32]),
     "ptSetBasicRendererRoundBatch": (_i32, [_vp, _u32]),
@@ -257,10 +258,12 @@ HIP_API = {
     "ptSceneStackNeeded": (_i32, [_vp, C.POINTER(C.c_uint32)]),
     "ptSetProfiling": (_i32, [_vp, _i32]),
     "ptGetKernelStats": (_i32, [_vp, _i32, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
+    "ptGetKernelRounds": (_i32, [_vp, _i32, C.POINTER(C.c_uint64)]),
     "ptResetKernelStats": (_i32, [_vp]),
     "ptCommGetUniqueId": (_i32, [C.POINTER(C.c_uint8)]),
     "ptCommCreate": (_vp, [_vp, _i32, _i32, C.POINTER(C.c_uint8)]),
     "ptCommDestroy": (None, [_vp]),
+    "ptCommSetTimeout": (_i32, [_vp, C.c_double]),
     "ptCommReduceSampleBuffer": (_i32, [_vp, _vp, _vp, _i32]),
     "ptCommGatherSampleBuffer": (_i32, [_vp, _vp, _vp, _i32]),
     "ptCommReduceSampleBufferInto": (_i32, [_vp, _vp, _vp, _vp, _i32]),

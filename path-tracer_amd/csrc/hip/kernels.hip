@@ -32,6 +32,54 @@
 
 namespace ptd {
 
+// --- shade branch statistics (experiment build only) ---------------------------
+//
+// Built with -DPT_SHADE_STATS=1 (tools/shade_stats.py via tools/build_variant.py),
+// each mark ShadeMark(k) records, once per wave that reaches it, the number of
+// lanes active there: waves[k] and lanes[k] summed over the launch, so
+// lanes[k] / waves[k] is the SIMD occupancy of that branch of Scatter.  The
+// product build compiles every mark to nothing.
+#ifndef PT_SHADE_STATS
+#define PT_SHADE_STATS 0
+#endif
+enum : uint32_t {
+    SM_ENTRY, SM_HIT, SM_ESCAPE, SM_MEDIUM_EVENT, SM_SURFACE, SM_REAL, SM_LIGHT, SM_LIGHT_BELOW,
+    SM_DIFFUSE_COSINE, SM_DIFFUSE_EVAL, SM_METAL_EVAL, SM_METAL_SAMPLE, SM_TRANS_EVAL, SM_TRANS_SAMPLE,
+    SM_TRANS_REFLECT, SM_TRANS_REFRACT, SM_OPENPBR, SM_NOT_REAL, SM_ROULETTE, SM_COMPLETED, SM_CONTINUE,
+    SM_EXTERIOR_MEDIUM, SM_MESH_HIT, SM_SPHERE_HIT, SM_CUBE_HIT, SM_PLANE_HIT, SM_COUNT
+};
+#if PT_SHADE_STATS
+__device__ unsigned long long g_shade_stats[2 * 32];
+PT_DEV uint32_t* ShadeStatLds()
+{
+    __shared__ uint32_t a[2 * 32];
+    return a;
+}
+PT_DEV void ShadeMark(uint32_t k)
+{
+    const uint64_t m = __ballot(1);
+    const uint32_t first = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+    if ((threadIdx.x & 63u) == first) {
+        atomicAdd(&ShadeStatLds()[2 * k], 1u);
+        atomicAdd(&ShadeStatLds()[2 * k + 1], (uint32_t)__popcll(m));
+    }
+}
+PT_DEV void ShadeStatsBegin()
+{
+    if (threadIdx.x < 64) ShadeStatLds()[threadIdx.x] = 0;
+    __syncthreads();
+}
+PT_DEV void ShadeStatsEnd()
+{
+    __syncthreads();
+    if (threadIdx.x < 2 * SM_COUNT) atomicAdd(&g_shade_stats[threadIdx.x], (unsigned long long)ShadeStatLds()[threadIdx.x]);
+}
+#else
+PT_DEV void ShadeMark(uint32_t) {}
+PT_DEV void ShadeStatsBegin() {}
+PT_DEV void ShadeStatsEnd() {}
+#endif
+
 // --- slot / pixel mapping ---------------------------------------------------
 
 // t / tiles_x by the host-computed reciprocal (exact for t * tiles_x < 2^32).
@@ -73,42 +121,49 @@ PT_DEV uint32_t HitPos(const dslots& L, uint32_t s, uint32_t p16) { return (s & 
 
 struct bsdf_parameters { uint32_t MaterialIndex; pt2 TextureUV; pt4 Lambda; pt4 ExteriorIOR; };
 
-PT_DEV bool Diffuse_Evaluate(const dscene& S, const bsdf_parameters& P, pt3 In, pt4& T, pt4& Pr)
+// The basic BSDFs (basic_diffuse / basic_metal / basic_translucent.glsl.inc)
+// take their material parameters already fetched (bsdf_material, below):
+// SampleSurfaceIntegrand reads them once per hit, in code shared by the
+// material types and by the light-sample evaluation and the BSDF sample,
+// instead of once in each of those divergent branches.  The expressions are
+// the reference's, so the results are the same bits.
+
+// Texture-able material parameters of a basic material (MaterialEvaluateBSDF /
+// MaterialSampleBSDF's *_GetParameters): Refl = the base reflectance
+// (diffuse / metal), Aux = the metal's specular reflectance or the
+// translucent's relative IOR, A / Rough = the GGX alpha of metal and
+// translucent materials.
+static_assert(PT_BASIC_DIFFUSE_BASE_SPECTRUM == PT_BASIC_METAL_BASE_SPECTRUM, "shared base reflectance word");
+struct bsdf_material {
+    pt4 Refl, Aux;
+    pt2 A;
+    bool Rough;
+};
+
+PT_DEV bool Diffuse_Evaluate(const bsdf_material& Q, pt3 In, pt4& T, pt4& Pr)
 {
-    pt4 R = MaterialTexturableReflectance(S, P.MaterialIndex, PT_BASIC_DIFFUSE_BASE_SPECTRUM, P.Lambda, P.TextureUV);
     Pr = v4s(In.z / PT_PI);
-    T = Pr * R;
+    T = Pr * Q.Refl;
     return true;
 }
 
-PT_DEV void Metal_GetParameters(const dscene& S, const bsdf_parameters& P, pt4& Base, pt4& Spec, pt2& A, bool& Rough)
+PT_DEV bool Metal_Evaluate(const bsdf_material& Q, pt3 In, pt3 Out, pt4& T, pt4& Pr)
 {
-    Base = MaterialTexturableReflectance(S, P.MaterialIndex, PT_BASIC_METAL_BASE_SPECTRUM, P.Lambda, P.TextureUV);
-    Spec = MaterialTexturableReflectance(S, P.MaterialIndex, PT_BASIC_METAL_SPECULAR_SPECTRUM, P.Lambda, P.TextureUV);
-    A = GGXRoughnessAlpha(MaterialTexturableValue(S, P.MaterialIndex, PT_BASIC_METAL_ROUGHNESS, P.TextureUV),
-                          MaterialTexturableValue(S, P.MaterialIndex, PT_BASIC_METAL_ROUGHNESS_ANISOTROPY, P.TextureUV));
-    Rough = A.x * A.y > PT_EPSILON;
-}
-
-PT_DEV bool Metal_Evaluate(const dscene& S, const bsdf_parameters& P, pt3 In, pt3 Out, pt4& T, pt4& Pr)
-{
-    pt4 Base, Spec; pt2 A; bool Rough;
-    Metal_GetParameters(S, P, Base, Spec, A, Rough);
-    if (In.z <= 0.0f || Out.z <= 0.0f || !Rough) return false;
+    const pt2 A = Q.A;
+    if (In.z <= 0.0f || Out.z <= 0.0f || !Q.Rough) return false;
     pt3 Half = SafeNormalize(In + Out);
     float Gm = GGXSmithG1(In, A);
     float D = GGXDistribution(Half, A);
     Pr = v4s(Gm * D / (4 * In.z));
     float Gs = GGXSmithG1(Out, A);
-    pt4 F = SchlickFresnelMetal(Base, Spec, dot(In, Half));
+    pt4 F = SchlickFresnelMetal(Q.Refl, Q.Aux, dot(In, Half));
     T = Pr * Gs * F;
     return true;
 }
 
-PT_DEV bool Metal_Sample(const dscene& S, rng& G, const bsdf_parameters& P, pt3 In, pt3& Out, pt4& T, pt4& Pr)
+PT_DEV bool Metal_Sample(rng& G, const bsdf_material& Q, pt3 In, pt3& Out, pt4& T, pt4& Pr)
 {
-    pt4 Base, Spec; pt2 A; bool Rough;
-    Metal_GetParameters(S, P, Base, Spec, A, Rough);
+    const pt2 A = Q.A;
     if (In.z <= 0.0f) return false;
     float U1 = G.R01();
     float U2 = G.R01();
@@ -117,33 +172,25 @@ PT_DEV bool Metal_Sample(const dscene& S, rng& G, const bsdf_parameters& P, pt3 
     Out = 2 * CosThetaIn * N - In;
     if (Out.z <= 0.0f) return false;
     Pr = v4s(1.0f);
-    if (Rough) {
+    if (Q.Rough) {
         float Gm = GGXSmithG1(In, A);
         float D = GGXDistribution(N, A);
         Pr = Pr * v4s(Gm * D / (4 * In.z));
     }
     float Gs = GGXSmithG1(Out, A);
-    pt4 F = SchlickFresnelMetal(Base, Spec, CosThetaIn);
+    pt4 F = SchlickFresnelMetal(Q.Refl, Q.Aux, CosThetaIn);
     T = Pr * Gs * F;
     return true;
 }
 
-PT_DEV void Translucent_GetParameters(const dscene& S, const bsdf_parameters& P, pt3 In, pt4& RelIOR, pt2& A, bool& Rough)
+// Q.Aux = RelativeIOR: Interior / Exterior when In.z < 0, else Exterior /
+// Interior (basic_translucent.glsl.inc GetParameters), In the direction
+// towards the viewer (Scatter's Out).
+PT_DEV bool Translucent_Evaluate(const bsdf_material& Q, pt3 In, pt3 Out, pt4& T, pt4& Pr)
 {
-    pt4 Interior = CauchyEmpiricalIOR(MFloat(S, P.MaterialIndex, PT_BASIC_TRANSLUCENT_IOR),
-                                      MFloat(S, P.MaterialIndex, PT_BASIC_TRANSLUCENT_ABBE_NUMBER), P.Lambda);
-    if (In.z < 0.0f) RelIOR = Interior / P.ExteriorIOR;
-    else RelIOR = P.ExteriorIOR / Interior;
-    A = GGXRoughnessAlpha(MaterialTexturableValue(S, P.MaterialIndex, PT_BASIC_TRANSLUCENT_ROUGHNESS, P.TextureUV),
-                          MaterialTexturableValue(S, P.MaterialIndex, PT_BASIC_TRANSLUCENT_ROUGHNESS_ANISOTROPY, P.TextureUV));
-    Rough = A.x * A.y > PT_EPSILON;
-}
-
-PT_DEV bool Translucent_Evaluate(const dscene& S, const bsdf_parameters& P, pt3 In, pt3 Out, pt4& T, pt4& Pr)
-{
-    pt4 RelIOR; pt2 A; bool Rough;
-    Translucent_GetParameters(S, P, In, RelIOR, A, Rough);
-    if (!Rough) { Pr = v4s(0.0f); T = v4s(0.0f); return true; }
+    const pt4 RelIOR = Q.Aux;
+    const pt2 A = Q.A;
+    if (!Q.Rough) { Pr = v4s(0.0f); T = v4s(0.0f); return true; }
     float Gm = GGXSmithG1(In, A);
     if (In.z * Out.z > 0) {
         pt3 Half = SafeNormalize(Out + In);
@@ -173,10 +220,10 @@ PT_DEV bool Translucent_Evaluate(const dscene& S, const bsdf_parameters& P, pt3 
     return true;
 }
 
-PT_DEV bool Translucent_Sample(const dscene& S, rng& G, const bsdf_parameters& P, pt3 In, pt3& Out, pt4& T, pt4& Pr)
+PT_DEV bool Translucent_Sample(rng& G, const bsdf_material& Q, pt3 In, pt3& Out, pt4& T, pt4& Pr)
 {
-    pt4 RelIOR; pt2 A; bool Rough;
-    Translucent_GetParameters(S, P, In, RelIOR, A, Rough);
+    const pt4 RelIOR = Q.Aux;
+    const pt2 A = Q.A;
     float U1 = G.R01();
     float U2 = G.R01();
     pt3 N = GGXVisibleNormal(In * pt_sign(In.z), A, U1, U2);
@@ -184,11 +231,12 @@ PT_DEV bool Translucent_Sample(const dscene& S, rng& G, const bsdf_parameters& P
     float CosThetaRefracted = ComputeCosThetaRefracted(RelIOR.x, CosThetaIn);
     float Reflectance = FresnelDielectric(RelIOR.x, CosThetaIn, CosThetaRefracted);
     if (G.R01() < Reflectance) {
+        ShadeMark(SM_TRANS_REFLECT);
         Out = 2 * CosThetaIn * N - In;
         if (Out.z * In.z <= 0) return false;
         pt4 F = FresnelDielectric(RelIOR, v4s(CosThetaIn));
         Pr = F;
-        if (Rough) {
+        if (Q.Rough) {
             float Gm = GGXSmithG1(In, A);
             float D = GGXDistribution(N, A);
             Pr = Pr * (Gm * D / (4 * pt_abs(In.z)));
@@ -197,9 +245,10 @@ PT_DEV bool Translucent_Sample(const dscene& S, rng& G, const bsdf_parameters& P
         T = Pr * Gs;
         return true;
     }
+    ShadeMark(SM_TRANS_REFRACT);
     Out = (CosThetaRefracted + RelIOR.x * CosThetaIn) * N - RelIOR.x * In;
     if (Out.z * In.z >= 0) return false;
-    if (Rough) {
+    if (Q.Rough) {
         pt3 N2 = SafeNormalize(Out + In * RelIOR.y);
         pt3 N3 = SafeNormalize(Out + In * RelIOR.z);
         pt3 N4 = SafeNormalize(Out + In * RelIOR.w);
@@ -469,61 +518,90 @@ PT_DEV medium ResolveMedium(const dscene& S, uint32_t ShapeIndex, pt4 Lambda)
     return Md;
 }
 
-template <uint32_t MATS>
-PT_DEV bool HasDirac(const dscene& S, const bsdf_parameters& P, uint32_t Type)
-{
-    if ((MATS & PT_MATS_METAL) && Type == PT_MATERIAL_TYPE_BASIC_METAL)
-        return MaterialTexturableValue(S, P.MaterialIndex, PT_BASIC_METAL_ROUGHNESS, P.TextureUV) < 1e-3f;
-    if ((MATS & PT_MATS_TRANSLUCENT) && Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT)
-        return MaterialTexturableValue(S, P.MaterialIndex, PT_BASIC_TRANSLUCENT_ROUGHNESS, P.TextureUV) < 1e-3f;
-    if ((MATS & PT_MATS_OPENPBR) && Type == PT_MATERIAL_TYPE_OPENPBR) return true;   // sampling only
-    return false;
-}
-
-// SampleSurfaceIntegrand (basic_scatter.glsl:68-109)
+// SampleSurfaceIntegrand (basic_scatter.glsl:68-109).  The material's
+// parameters are fetched once, in code shared by the types: the metal and
+// translucent roughness / anisotropy (HasDirac reads the same roughness
+// value) before the light choice, the reflectances after the sampled
+// direction is known (a sky sample below the surface ends the path first).
 template <uint32_t MATS>
 PT_DEV bool SampleSurfaceIntegrand(const dscene& S, rng& G, pt3 Nrm, pt3 TX, pt3 TY, const bsdf_parameters& P, pt3 Out,
                                    pt3& In, pt4& Throughput, pt4& Probability)
 {
-    uint32_t Type = MUint(S, P.MaterialIndex, 0);
-    float LightProbability = HasDirac<MATS>(S, P, Type) ? 0.0f : S.g.SkyboxSamplingProbability;
+    const uint32_t M = P.MaterialIndex;
+    const uint32_t Type = MUint(S, M, 0);
+    const bool diffuse = (MATS & PT_MATS_DIFFUSE) && Type == PT_MATERIAL_TYPE_BASIC_DIFFUSE;
+    const bool metal = (MATS & PT_MATS_METAL) && Type == PT_MATERIAL_TYPE_BASIC_METAL;
+    const bool trans = (MATS & PT_MATS_TRANSLUCENT) && Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT;
+    const bool openpbr = (MATS & PT_MATS_OPENPBR) && Type == PT_MATERIAL_TYPE_OPENPBR;
+    bsdf_material Q;
+    Q.Rough = false;
+    // HasDirac (basic_metal / basic_translucent .glsl.inc: roughness < 1e-3;
+    // OpenPBR: sampling only, HasDirac true).
+    bool Dirac = openpbr;
+    if ((MATS & (PT_MATS_METAL | PT_MATS_TRANSLUCENT)) && (metal || trans)) {
+        const float Roughness = MaterialTexturableValue(
+            S, M, metal ? PT_BASIC_METAL_ROUGHNESS : PT_BASIC_TRANSLUCENT_ROUGHNESS, P.TextureUV);
+        const float Anisotropy = MaterialTexturableValue(
+            S, M, metal ? PT_BASIC_METAL_ROUGHNESS_ANISOTROPY : PT_BASIC_TRANSLUCENT_ROUGHNESS_ANISOTROPY, P.TextureUV);
+        Q.A = GGXRoughnessAlpha(Roughness, Anisotropy);
+        Q.Rough = Q.A.x * Q.A.y > PT_EPSILON;
+        Dirac = Roughness < 1e-3f;
+    }
+    float LightProbability = Dirac ? 0.0f : S.g.SkyboxSamplingProbability;
     pt4 MaterialPDF = v4s(0.0f);
     pt3 SMD = v3(S.g.SkyboxMeanDirection[0], S.g.SkyboxMeanDirection[1], S.g.SkyboxMeanDirection[2]);
     pt3 Mu = v3(dot(SMD, TX), dot(SMD, TY), dot(SMD, Nrm));
     bool ok;
     const bool light = G.R01() < LightProbability;
-    const bool diffuse = (MATS & PT_MATS_DIFFUSE) && Type == PT_MATERIAL_TYPE_BASIC_DIFFUSE;
     // A diffuse hit draws In by the light choice -- the sky lobe or the
     // material's cosine sample -- and then evaluates the material with the
     // same arguments either way (MaterialEvaluateBSDF / MaterialSampleBSDF of
-    // basic_diffuse.glsl.inc), so the evaluation (texture + spectrum) runs
-    // once after the join instead of in both divergent halves.
+    // basic_diffuse.glsl.inc), so the evaluation runs once after the join.
     if (light) {
+        ShadeMark(SM_LIGHT);
         In = RandomVonMisesFisher(G, vmf_consts{S.vmf_inv_kappa, S.vmf_exp_m2k, S.vmf_norm}, Mu);
-        if (In.z < 0.0f) return false;
+        if (In.z < 0.0f) { ShadeMark(SM_LIGHT_BELOW); return false; }
     } else if (diffuse) {
+        ShadeMark(SM_DIFFUSE_COSINE);
         In = SafeNormalize(RandomDirection(G) + v3(0, 0, 1));
     }
+    // Reflectances: the diffuse and metal base spectrum share a material word
+    // (BASE_SPECTRUM = 1), the metal's specular spectrum; the translucent's
+    // Cauchy IOR relative to the exterior on Out's side.
+    if (diffuse || metal) Q.Refl = MaterialTexturableReflectance(S, M, PT_BASIC_METAL_BASE_SPECTRUM, P.Lambda, P.TextureUV);
+    if (metal) Q.Aux = MaterialTexturableReflectance(S, M, PT_BASIC_METAL_SPECULAR_SPECTRUM, P.Lambda, P.TextureUV);
+    if (trans) {
+        pt4 Interior = CauchyEmpiricalIOR(MFloat(S, M, PT_BASIC_TRANSLUCENT_IOR),
+                                          MFloat(S, M, PT_BASIC_TRANSLUCENT_ABBE_NUMBER), P.Lambda);
+        if (Out.z < 0.0f) Q.Aux = Interior / P.ExteriorIOR;
+        else Q.Aux = P.ExteriorIOR / Interior;
+    }
     if (diffuse) {
-        ok = Diffuse_Evaluate(S, P, Out, Throughput, MaterialPDF);
+        ShadeMark(SM_DIFFUSE_EVAL);
+        ok = Diffuse_Evaluate(Q, Out, Throughput, MaterialPDF);
         if (!ok) return false;
     } else if (light) {
         // MaterialEvaluateBSDF(Parameters, Out, In, ...)
-        if ((MATS & PT_MATS_METAL) && Type == PT_MATERIAL_TYPE_BASIC_METAL)
-            ok = Metal_Evaluate(S, P, Out, In, Throughput, MaterialPDF);
-        else if ((MATS & PT_MATS_TRANSLUCENT) && Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT)
-            ok = Translucent_Evaluate(S, P, Out, In, Throughput, MaterialPDF);
-        else ok = false;
+        if (metal) {
+            ShadeMark(SM_METAL_EVAL);
+            ok = Metal_Evaluate(Q, Out, In, Throughput, MaterialPDF);
+        } else if (trans) {
+            ShadeMark(SM_TRANS_EVAL);
+            ok = Translucent_Evaluate(Q, Out, In, Throughput, MaterialPDF);
+        } else ok = false;
         if (!ok) return false;
     } else {
         // MaterialSampleBSDF(Parameters, Out, In, ...)
-        if ((MATS & PT_MATS_METAL) && Type == PT_MATERIAL_TYPE_BASIC_METAL) {
-            ok = Metal_Sample(S, G, P, Out, In, Throughput, MaterialPDF);
-        } else if ((MATS & PT_MATS_TRANSLUCENT) && Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT) {
-            ok = Translucent_Sample(S, G, P, Out, In, Throughput, MaterialPDF);
-        } else if ((MATS & PT_MATS_OPENPBR) && Type == PT_MATERIAL_TYPE_OPENPBR) {
-            openpbr_parameters Q = OpenPBR_Parameters(S, G, P);
-            ok = OpenPBR_Sample(G, Q, Out, In, Throughput, MaterialPDF);
+        if (metal) {
+            ShadeMark(SM_METAL_SAMPLE);
+            ok = Metal_Sample(G, Q, Out, In, Throughput, MaterialPDF);
+        } else if (trans) {
+            ShadeMark(SM_TRANS_SAMPLE);
+            ok = Translucent_Sample(G, Q, Out, In, Throughput, MaterialPDF);
+        } else if (openpbr) {
+            ShadeMark(SM_OPENPBR);
+            openpbr_parameters O = OpenPBR_Parameters(S, G, P);
+            ok = OpenPBR_Sample(G, O, Out, In, Throughput, MaterialPDF);
         } else {
             ok = false;
         }
@@ -664,60 +742,6 @@ PT_DEV void TileOrderStoreRay(const dslots& L, uint32_t s, bool valid, pt3 O, pt
     L.slotof[q] = (uint8_t)(s & 255u);
 }
 
-// --- Global ray sort ---------------------------------------------------------
-//
-// TileOrder sorts a tile's 256 new rays by direction octant; the global sort
-// orders ALL of a frame's rays by (octant, Morton cell of the origin in a
-// 16^3 grid over the scene's bounds) before each extend, so a wave traces
-// rays that start in the same region in the same octant wherever their
-// pixels are.  Measured on C3's settled rays (tools/exp_reorder.py,
-// profiles/r03_reorder): with longest-first block dispatch the traversal of
-// the sorted order takes 0.76x that of the tile-octant order (SIMD efficiency
-// 0.53 -> 0.67; per-ray step counts do not depend on the order, so the hits
-// are identical).  Path state stays per slot (pixel tiles); only the rays
-// move: raygen / shade write each new ray by slot with its key and count the
-// key; at the next round's start a scan turns the counts into bin offsets and
-// a scatter gives every position its slot (perm); extend traces position q
-// = the ray of slot perm[q] and stores the hit by slot, where shade reads it.
-PT_DEV uint32_t MortonSpread3(uint32_t v)   // 3 bits -> every third bit
-{
-    v &= 7u;
-    return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4);
-}
-
-// Sort key (12 bits): direction octant, then the origin's cell of an 8^3 grid
-// over the TLAS root box in Morton order.  The root box bounds every shape
-// (a scene without shapes reads the zeroed placeholder node: every origin
-// lands in cell 0).  Key choice: tools/exp_gsort.py (profiles/r03_gsort).
-// Two direction bits more (14-bit keys, 16384 bins) made the traversal
-// faster in that experiment (0.80x vs 0.89x of the tile-order layout) but
-// in the renderer extend only 0.88x, while the count / scan / scatter pass
-// grew from 34 to 52 us; not kept.
-PT_DEV uint32_t RayKey(const dscene& S, pt3 O, pt3 V)
-{
-    float4 a = S.shape_nodes[0], b = S.shape_nodes[1];
-    float sx = 8.0f / fmaxf(b.x - a.x, 1e-30f), sy = 8.0f / fmaxf(b.y - a.y, 1e-30f), sz = 8.0f / fmaxf(b.z - a.z, 1e-30f);
-    uint32_t cx = (uint32_t)fminf(fmaxf((O.x - a.x) * sx, 0.0f), 7.0f);
-    uint32_t cy = (uint32_t)fminf(fmaxf((O.y - a.y) * sy, 0.0f), 7.0f);
-    uint32_t cz = (uint32_t)fminf(fmaxf((O.z - a.z) * sz, 0.0f), 7.0f);
-    uint32_t oct = (V.x < 0.0f ? 1u : 0u) | (V.y < 0.0f ? 2u : 0u) | (V.z < 0.0f ? 4u : 0u);
-    return (oct << 9) | MortonSpread3(cx) | (MortonSpread3(cy) << 1) | (MortonSpread3(cz) << 2);
-}
-
-// A new ray of slot s in global-sort mode: stored by slot with its key (the
-// next round's sort pass counts and places it).  (Counting here instead, a
-// ballot per distinct key of the wave and one returning atomic per group
-// into key counters split over 8 tile classes, removed the count kernel
-// (9.8 us) but cost shade 13 us and raygen 48 us on C3: the camera rays'
-// few keys still queue their atomics; a single counter per key cost shade
-// 114 us.)
-PT_DEV void GlobalSortStoreRay(const dscene& S, const dslots& L, uint32_t s, bool valid, pt3 O, pt3 V)
-{
-    if (!valid) return;
-    L.ray[s] = make_float4(O.x, O.y, O.z, __uint_as_float(PackUnitVector(V)));
-    L.key[s] = (uint16_t)RayKey(S, O, V);
-}
-
 // GenerateNewPath (basic_scatter.glsl:7-42) + GenerateCameraRay (scene.glsl.inc:613-655)
 PT_DEV void GenerateNewPath(const dscene& S, const dslots& L, const dframe& F, const dparams& Pm, rng& G, uint32_t s,
                             uint32_t x, uint32_t y, pt3& RO, pt3& RV, bool act_none = false)
@@ -791,6 +815,7 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
 
     if (HitTime >= ScatteringTime) {
         if (ScatteringTime < PT_HIT_TIME_LIMIT) {
+            ShadeMark(SM_MEDIUM_EVENT);
             O = O + V * ScatteringTime;
             pt3 X, Y, Z = V;
             ComputeCoordinateFrame(Z, X, Y);
@@ -803,6 +828,7 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
             Path.Probability = Path.Probability * Density;
             V = normalize(X * Sc.x + Y * Sc.y + Z * Sc.z);
         } else {
+            ShadeMark(SM_ESCAPE);
             pt4 Emission = SampleSkyboxRadiance(S, V, Lambda);
             float ClusterPDF = Path.Probability.x + Path.Probability.y + Path.Probability.z + Path.Probability.w;
             pt4 E = Emission * Path.Throughput;
@@ -820,6 +846,7 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
         return max4(Path.Probability) > PT_EPSILON;
     }
 
+    ShadeMark(SM_SURFACE);
     pt3 Nrm = UnpackUnitVector(PN);
     pt3 TX = UnpackUnitVector(PT);
     pt3 TY = cross(Nrm, TX);
@@ -835,6 +862,7 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
     } else {
         IsReal = Md.Priority == ShapePriority;
         if (IsReal) {
+            ShadeMark(SM_EXTERIOR_MEDIUM);
             uint32_t Ext = SHAPE_INDEX_NONE;
             for (int I = 0; I < 4; I++) {
                 if (Path.Active[I] == Active) continue;
@@ -846,6 +874,7 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
 
     pt3 In;
     if (IsReal) {
+        ShadeMark(SM_REAL);
         bsdf_parameters P;
         P.MaterialIndex = HitMaterial;
         P.TextureUV = UV;
@@ -857,6 +886,7 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
         Path.Throughput = Path.Throughput * (T * Scale);
         Path.Probability = Path.Probability * (Pr * Scale);
     } else {
+        ShadeMark(SM_NOT_REAL);
         In = -Out;
     }
 
@@ -878,6 +908,7 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
         }
     }
 
+    ShadeMark(SM_ROULETTE);
     if (G.R01() < PTP) return false;
     Path.Probability = Path.Probability * (1.0f - PTP);
 
@@ -910,8 +941,7 @@ __global__ __launch_bounds__(256) void raygen_kernel(dscene S, dslots L, dframe 
         GenerateNewPath(S, L, F, Pm, G, s, x, y, O, V);
         F.accum[(size_t)y * F.width + x] = make_float4(0, 0, 0, 0);
     }
-    if (L.gsort) GlobalSortStoreRay(S, L, s, valid, O, V);
-    else TileOrderStoreRay(L, s, valid, O, V, L.pos[s] & 255u);
+    TileOrderStoreRay(L, s, valid, O, V, L.pos[s] & 255u);
 }
 
 // Ray sources of the extend kernel: the renderer's slots, or the arrays of
@@ -976,53 +1006,8 @@ struct ray_source_arrays {
     }
 };
 
-// Global ray sort: position q < *nvalid traces the ray of slot perm[q] and
-// leaves its hit and outcome class at q.
-struct ray_source_sorted {
-    dslots L;
-    dframe F;
-    PT_DEV bool load(uint32_t q, pt3& O, pt3& V, float& D) const
-    {
-        if (q >= *L.nvalid) return false;
-        float4 r = L.ray[L.perm[q]];
-        O = v3(r.x, r.y, r.z);
-        V = UnpackUnitVector(__float_as_uint(r.w));
-        D = PT_HIT_TIME_LIMIT;
-        return true;
-    }
-    // The hit and its outcome class go to the ray's SLOT (perm[q], re-read:
-    // an L1 hit), so shade reads them coalesced; extend's scattered stores
-    // cost less than shade's scattered loads did.
-    PT_DEV void store(uint32_t q, const lane_state& Ln, bool vidx21) const
-    {
-        uint32_t s = L.perm[q];
-        L.hit[s] = CompactHit(Ln, vidx21);
-        L.uv[s] = make_float2(Ln.C.y, Ln.C.z);
-    }
-    PT_DEV void outcome(uint32_t q, uint32_t cls, bool) const { L.cls[L.perm[q]] = (uint8_t)cls; }
-};
-
-// Diagnostics in global-sort mode (ptExtendStats): slot s's current ray,
-// traced without storing anything (the next Run's sort decides positions).
-struct ray_source_slot_rays {
-    dslots L;
-    dframe F;
-    PT_DEV bool load(uint32_t s, pt3& O, pt3& V, float& D) const
-    {
-        uint32_t x, y;
-        if (!SlotPixel(F, s, x, y)) return false;
-        float4 r = L.ray[s];
-        O = v3(r.x, r.y, r.z);
-        V = UnpackUnitVector(__float_as_uint(r.w));
-        D = PT_HIT_TIME_LIMIT;
-        return true;
-    }
-    PT_DEV void store(uint32_t, const lane_state&, bool) const {}
-    PT_DEV void outcome(uint32_t, uint32_t, bool) const {}
-};
-
 template <class Src>
-constexpr bool kRendererSource = std::is_same<Src, ray_source_slots>::value || std::is_same<Src, ray_source_sorted>::value;
+constexpr bool kRendererSource = std::is_same<Src, ray_source_slots>::value;
 
 // Extend: one ray per thread, LaneStep run to completion.  (A persistent
 // variant with per-wave dynamic ray fetch was measured 1.6x slower on C3: the
@@ -1111,12 +1096,7 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
     // kernel's tail holds short blocks; each wave records its own time.
     uint32_t tile = blockIdx.x;
     bool timed = false;
-    if constexpr (std::is_same<Src, ray_source_sorted>::value) {
-        // Global sort: block b traces positions [256b, 256b + 256), which the
-        // sort pass filled longest-first; the wave times feed the next scan.
-        timed = src.L.gcost != 0;
-    } else if constexpr (kRendererSource<Src>) {
-        tile += src.L.tile_base;
+    if constexpr (kRendererSource<Src>) {
         if (src.L.order) {
             tile = src.L.order[blockIdx.x];
             timed = true;
@@ -1129,10 +1109,8 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
 // wave's time, descending, by a one-block counting sort over 512 log-spaced
 // buckets (16 per octave).  Any order gives the same results; only the
 // kernel's tail changes.
-__global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, uint32_t* order, uint32_t base,
-                                                          uint32_t tiles)
+__global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, uint32_t* order, uint32_t tiles)
 {
-    cost += 4 * (size_t)base;
     __shared__ uint32_t count[512];
     for (uint32_t i = threadIdx.x; i < 512; i += 1024) count[i] = 0;
     __syncthreads();
@@ -1167,7 +1145,7 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, 
         count[threadIdx.x] = before + incl - c;
     }
     __syncthreads();
-    for (uint32_t t = threadIdx.x; t < tiles; t += 1024) order[atomicAdd(&count[key(t)], 1u)] = base + t;
+    for (uint32_t t = threadIdx.x; t < tiles; t += 1024) order[atomicAdd(&count[key(t)], 1u)] = t;
 }
 
 // Mesh vertices decoded once per upload for HitAttributes: the octahedral
@@ -1205,232 +1183,6 @@ __global__ __launch_bounds__(256) void zero_unowned_kernel(float4* accum, uint32
         if (((y >> 4) % nranks) == rank) continue;
         for (uint32_t x = blockIdx.x * 256 + threadIdx.x; x < width; x += gridDim.x * 256)
             accum[(size_t)y * width + x] = make_float4(0, 0, 0, 0);
-    }
-}
-
-constexpr uint32_t GS_CHUNK = 8192;   // slots per block of the count / scatter kernels
-constexpr uint32_t GS_THREADS = 1024; // (8 slots per thread; 16 waves per block hide the atomics' latency)
-
-PT_DEV uint32_t GsKey(const dslots& L, const dframe& F, uint32_t s)
-{
-    uint32_t x, y;
-    return SlotPixel(F, s, x, y) ? (uint32_t)L.key[s] : PT_GS_BINS;
-}
-
-// Block-wide (GS_THREADS) exclusive scan: returns the sum of v over the
-// threads before this one; *total (every thread) = the sum over all.
-template <class T>
-PT_DEV T GsBlockScan(T v, T* wsum, T* total)
-{
-    const uint32_t t = threadIdx.x;
-    T incl = v;
-    for (int o = 1; o < 64; o <<= 1) {
-        T u = __shfl_up(incl, o, 64);
-        if ((t & 63u) >= (uint32_t)o) incl += u;
-    }
-    if ((t & 63u) == 63u) wsum[t >> 6] = incl;
-    __syncthreads();
-    T before = 0, all = 0;
-    for (uint32_t w = 0; w < GS_THREADS / 64; w++) {
-        before += w < (t >> 6) ? wsum[w] : T(0);
-        all += wsum[w];
-    }
-    __syncthreads();   // wsum reusable
-    *total = all;
-    return before + incl - v;
-}
-
-// Longest-first bin order (dslots::gcost).  A bin's cost is the mean extend
-// time over the positions its rays held in the previous round (binprev): the
-// extend blocks' times (the sum of a block's four wave times, one uint4 of
-// tilecost) as prefix sums in LDS over units of U blocks (at most GS_PREFIX
-// units), linearly interpolated inside a unit, bucketed like tile_order_kernel (16
-// buckets per octave; bins the previous round did not see go last).  Only
-// the bins that hold rays this round are ranked (about a quarter on C3).
-// tools/exp_bincost.py: on C3's settled rays this order traces in 0.70-0.74x
-// of slot order against 0.78-0.79x for key order with block-index
-// longest-first (profiles/r03_bincost).
-constexpr uint32_t GS_PREFIX = 8192;   // LDS prefix entries (32 KB)
-
-// The sort pass's scan (one block of GS_THREADS): cursor[b] = first position
-// of bin b (bins in key order, or longest first with gcost), cursor[PT_GS_BINS]
-// = *nvalid = all valid rays (slots outside the image follow); binprev
-// records the ranges for the next round; the counts cleared.  Every global
-// load is issued at the start (one memory latency), the rest runs in LDS.
-PT_DEV void GsScan(const dslots& L, uint32_t* cursor)
-{
-    constexpr uint32_t PER = PT_GS_BINS / GS_THREADS;
-    constexpr uint32_t PE = GS_PREFIX / GS_THREADS;   // prefix entries per thread
-    __shared__ uint32_t wsum[GS_THREADS / 64];
-    __shared__ float fsum[GS_THREADS / 64];
-    __shared__ uint32_t bucket[512];
-    __shared__ uint32_t byrank[PT_GS_BINS];
-    __shared__ float pre[GS_PREFIX + 1];
-    const uint32_t t = threadIdx.x, b0 = t * PER;
-    uint32_t cnt[PER], rank[PER];
-    uint2 pv[PER];
-#pragma unroll
-    for (uint32_t i = 0; i < PER; i++) {
-        cnt[i] = L.hist[b0 + i];
-        rank[i] = b0 + i;
-    }
-    if (L.gcost) {
-        // Units of U blocks (U = 1 while the frame has <= GS_PREFIX blocks).
-        const uint32_t nb = L.n / 256, U = (nb + GS_PREFIX - 1) / GS_PREFIX;
-        const uint32_t ne = (nb + U - 1) / U;
-        const uint4* tc = reinterpret_cast<const uint4*>(L.tilecost);
-        float v[PE];
-#pragma unroll
-        for (uint32_t j = 0; j < PE; j++) v[j] = 0;
-        for (uint32_t u = 0; u < U; u++) {
-#pragma unroll
-            for (uint32_t j = 0; j < PE; j++) {
-                const uint32_t blk = (t * PE + j) * U + u;
-                uint4 c = blk < nb ? tc[blk] : make_uint4(0, 0, 0, 0);
-                v[j] += (float)(c.x + c.y + c.z + c.w);
-            }
-        }
-#pragma unroll
-        for (uint32_t i = 0; i < PER; i++) pv[i] = L.binprev[b0 + i];
-        float sum = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < PE; j++) sum += v[j];
-        float all;
-        float run = GsBlockScan(sum, fsum, &all);
-#pragma unroll
-        for (uint32_t j = 0; j < PE; j++) {
-            pre[t * PE + j] = run;
-            run += v[j];
-        }
-        if (t == GS_THREADS - 1) pre[GS_PREFIX] = all;
-        for (uint32_t i = t; i < 512; i += GS_THREADS) bucket[i] = 0;
-        __syncthreads();
-        const float unit = 256.0f * (float)U;
-        auto at = [&](uint32_t p) -> float {
-            const uint32_t e = min(p / (256u * U), ne);
-            const float f = (float)(p - e * 256u * U) / unit;
-            const float a = pre[e];
-            return e < ne ? a + (pre[e + 1] - a) * f : a;
-        };
-        uint32_t key[PER];
-#pragma unroll
-        for (uint32_t i = 0; i < PER; i++) {
-            key[i] = 511u;
-            if (cnt[i] && pv[i].y) {
-                // mean time per wave of 64 positions
-                float c = (at(pv[i].x + pv[i].y) - at(pv[i].x)) / (float)pv[i].y * 64.0f;
-                if (c >= 16.0f) {
-                    uint32_t ci = (uint32_t)fminf(c, 4.0e9f);
-                    uint32_t e = 31u - __clz(ci);
-                    uint32_t m = (ci >> (e - 4)) & 15u;
-                    key[i] = 511u - min(e * 16u + m, 511u);
-                }
-            }
-            if (cnt[i]) atomicAdd(&bucket[key[i]], 1u);
-        }
-        __syncthreads();
-        uint32_t c = t < 512 ? bucket[t] : 0u, tot;
-        uint32_t start = GsBlockScan(c, wsum, &tot);
-        if (t < 512) bucket[t] = start;
-#pragma unroll
-        for (uint32_t i = 0; i < PER; i++) byrank[b0 + i] = 0;
-        __syncthreads();
-        // Rank inside a bucket by LDS atomic: any order of the bins gives the
-        // same results (only the dispatch order of the rays changes).  The
-        // empty bins take no rank (their cursor is never used).
-#pragma unroll
-        for (uint32_t i = 0; i < PER; i++) rank[i] = cnt[i] ? atomicAdd(&bucket[key[i]], 1u) : 0u;
-        __syncthreads();
-#pragma unroll
-        for (uint32_t i = 0; i < PER; i++)
-            if (cnt[i]) byrank[rank[i]] = cnt[i];
-    } else {
-#pragma unroll
-        for (uint32_t i = 0; i < PER; i++) byrank[rank[i]] = cnt[i];
-    }
-    // Counts by rank, their exclusive prefix sums, back to the bins.
-    __syncthreads();
-    uint32_t r[PER], sum = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < PER; i++) {
-        r[i] = byrank[b0 + i];
-        sum += r[i];
-    }
-    uint32_t total;
-    uint32_t run = GsBlockScan(sum, wsum, &total);
-#pragma unroll
-    for (uint32_t i = 0; i < PER; i++) {
-        byrank[b0 + i] = run;
-        run += r[i];
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t i = 0; i < PER; i++) {
-        uint32_t first = byrank[rank[i]];
-        cursor[b0 + i] = first;
-        L.binprev[b0 + i] = make_uint2(first, cnt[i]);
-        L.hist[b0 + i] = 0;
-    }
-    if (t == GS_THREADS - 1) { cursor[PT_GS_BINS] = total; *L.nvalid = total; }
-}
-
-// Global ray sort pass (before each extend), three launches over the key
-// bins (PT_GS_BINS + one for slots outside the image):
-//   gsort_count_kernel    per chunk of GS_CHUNK slots an LDS histogram of the
-//                         keys, one global add per nonzero bin;
-//   gsort_scan_kernel     the bins' first positions (GsScan: key order, or
-//                         longest first by the previous round's cost);
-//   gsort_scatter_kernel  per chunk again: each nonzero bin reserves its range
-//                         with one global atomic, each slot takes the next
-//                         position of its bin's range (LDS atomic) and
-//                         records itself there (perm).
-// (Copying the rays into sorted order instead of extend gathering them
-// through perm: scatter +8 us, shade +10 us, extend -6 us; not kept.)
-// Same-address global atomics per ray serialise badly (camera rays share one
-// key): every global atomic here is per (chunk, bin).
-__global__ __launch_bounds__(GS_THREADS) void gsort_count_kernel(dslots L, dframe F)
-{
-    __shared__ uint32_t cnt[PT_GS_BINS + 1];
-    for (uint32_t b = threadIdx.x; b <= PT_GS_BINS; b += GS_THREADS) cnt[b] = 0;
-    __syncthreads();
-    const uint32_t s0 = blockIdx.x * GS_CHUNK;
-#pragma unroll
-    for (uint32_t i = 0; i < GS_CHUNK / GS_THREADS; i++) {
-        uint32_t s = s0 + i * GS_THREADS + threadIdx.x;
-        if (s < L.n) atomicAdd(&cnt[GsKey(L, F, s)], 1u);
-    }
-    __syncthreads();
-    for (uint32_t b = threadIdx.x; b < PT_GS_BINS; b += GS_THREADS)
-        if (uint32_t c = cnt[b]) atomicAdd(&L.hist[b], c);
-}
-
-__global__ __launch_bounds__(GS_THREADS) void gsort_scan_kernel(dslots L, uint32_t* cursor) { GsScan(L, cursor); }
-
-__global__ __launch_bounds__(GS_THREADS) void gsort_scatter_kernel(dslots L, dframe F, uint32_t* cursor)
-{
-    // One LDS word per bin: the chunk's count, then (after the reservation)
-    // the next free position of the chunk's range in that bin.
-    __shared__ uint32_t cnt[PT_GS_BINS + 1];
-    for (uint32_t b = threadIdx.x; b <= PT_GS_BINS; b += GS_THREADS) cnt[b] = 0;
-    __syncthreads();
-    const uint32_t s0 = blockIdx.x * GS_CHUNK;
-    uint32_t k[GS_CHUNK / GS_THREADS];
-#pragma unroll
-    for (uint32_t i = 0; i < GS_CHUNK / GS_THREADS; i++) {
-        uint32_t s = s0 + i * GS_THREADS + threadIdx.x;
-        k[i] = s < L.n ? GsKey(L, F, s) : 0u;
-        if (s < L.n) atomicAdd(&cnt[k[i]], 1u);
-    }
-    __syncthreads();
-    for (uint32_t b = threadIdx.x; b <= PT_GS_BINS; b += GS_THREADS)
-        if (uint32_t c = cnt[b]) cnt[b] = atomicAdd(&cursor[b], c);
-    __syncthreads();
-#pragma unroll
-    for (uint32_t i = 0; i < GS_CHUNK / GS_THREADS; i++) {
-        uint32_t s = s0 + i * GS_THREADS + threadIdx.x;
-        if (s >= L.n) continue;
-        uint32_t q = atomicAdd(&cnt[k[i]], 1u);
-        if (k[i] < PT_GS_BINS) L.perm[q] = s;
     }
 }
 
@@ -1540,42 +1292,25 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
     // tile run the surface path or the escape path, mostly not both; path
     // state is read and written by slot (gathers within the tile's records).
     const uint32_t base = tile * 256;
-    uint32_t s, p16 = 0;
-    if (L.gsort) {
-        // Global ray sort: extend left each slot's outcome class by slot; the
-        // tile's class masks are built in LDS, then ShadeOrder as below.
-        __shared__ uint64_t gm[4 * PT_OUTCOME_CLASSES];
-        uint32_t c = L.cls[base | threadIdx.x];
-        uint32_t w = threadIdx.x >> 6;
-#pragma unroll
-        for (uint32_t k = 0; k < PT_OUTCOME_CLASSES; k++) {
-            uint64_t b = __ballot(c == k);
-            if ((threadIdx.x & 63u) == 0) gm[4 * k + w] = b;
-        }
-        __syncthreads();
-        const uint32_t pq = S.mat_classes ? ShadePosition(gm, threadIdx.x)
-                                          : ShadePosition2(gm + 4 * (PT_OUTCOME_CLASSES - 1), threadIdx.x);
-        s = base | pq;
-    } else {
 #if PT_SHADE_ORDER
-        // The position is the ray's own (slotof inverts TileOrder's slot ->
-        // position map), so the ray / hit / uv records load from it directly,
-        // beside the slotof lookup instead of after a pos[s] lookup.
-        const uint64_t* om = L.outcome + (size_t)tile * (4 * PT_OUTCOME_CLASSES);
-        const uint32_t pq = S.mat_classes ? ShadePosition(om, threadIdx.x)
-                                          : ShadePosition2(om + 4 * (PT_OUTCOME_CLASSES - 1), threadIdx.x);
-        s = base | L.slotof[base | pq];
-        p16 = pq << 8;   // RayPos(s, p16) == base | pq (shade -1 % vs gathering pos[s])
+    // The position is the ray's own (slotof inverts TileOrder's slot ->
+    // position map), so the ray / hit / uv records load from it directly,
+    // beside the slotof lookup instead of after a pos[s] lookup.
+    const uint64_t* om = L.outcome + (size_t)tile * (4 * PT_OUTCOME_CLASSES);
+    const uint32_t pq = S.mat_classes ? ShadePosition(om, threadIdx.x)
+                                      : ShadePosition2(om + 4 * (PT_OUTCOME_CLASSES - 1), threadIdx.x);
+    const uint32_t s = base | L.slotof[base | pq];
+    const uint32_t p16 = pq << 8;   // RayPos(s, p16) == base | pq (shade -1 % vs gathering pos[s])
 #else
-        s = base | threadIdx.x;
-        p16 = L.pos[s];
+    const uint32_t s = base | threadIdx.x;
+    const uint32_t p16 = L.pos[s];
 #endif
-    }
     uint32_t x, y;
     bool valid = SlotPixel(F, s, x, y);
     pt3 O = v3s(0), V = v3s(0);
     bool completed = false;
     if (valid) {
+        ShadeMark(SM_ENTRY);
         rng G;
         G.State = pt_seed(x, y, Pm.seed);
 
@@ -1597,7 +1332,7 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
         // (Trace, scene.glsl.inc:535-608) are rebuilt here and go through the
         // same octahedral snorm16 quantisation as the reference's
         // StoreTraceHit / LoadTraceResult.
-        uint32_t q = L.gsort ? s : RayPos(L, s, p16);
+        uint32_t q = RayPos(L, s, p16);
         float4 r = L.ray[q];
         O = v3(r.x, r.y, r.z);
         V = UnpackUnitVector(__float_as_uint(r.w));
@@ -1607,9 +1342,19 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
         uint32_t PN = 0, PTg = 0;
         pt2 UV = v2(0, 0);
         if (HitShape != SHAPE_INDEX_NONE) {
+            ShadeMark(SM_HIT);
+#if PT_SHADE_STATS
+            {
+                const int32_t Ty = S.shapes[HitShape].Type;
+                if (Ty == PT_SHAPE_TYPE_MESH_INSTANCE) ShadeMark(SM_MESH_HIT);
+                else if (Ty == PT_SHAPE_TYPE_SPHERE) ShadeMark(SM_SPHERE_HIT);
+                else if (Ty == PT_SHAPE_TYPE_PLANE) ShadeMark(SM_PLANE_HIT);
+                else ShadeMark(SM_CUBE_HIT);
+            }
+#endif
             float2 c = L.uv[q];
             pt3 N, TX;
-            HitAttributesRecord(S, HitShape, h, c, HitMaterial, N, TX, UV);
+            HitAttributesRecord(S, HitShape, h, c, HitMaterial, N, TX, UV, S.shape_uv[HitShape] != 0);
             HitMaterial &= 0xFFFFu;
             HitShape &= 0xFFFFu;
             HitTime = h.x;
@@ -1621,11 +1366,13 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
             // StorePathVertex of a continuing path: Scatter changes Sample only
             // on escape (which terminates the path) and never Lambda0, so lam
             // is unchanged; the active-shape stack is written when it moved.
+            ShadeMark(SM_CONTINUE);
             L.thr[s] = make_float4(P.Throughput.x, P.Throughput.y, P.Throughput.z, P.Throughput.w);
             L.prob[s] = make_float4(P.Probability.x, P.Probability.y, P.Probability.z, P.Probability.w);
             uint2 na = make_uint2((P.Active[1] << 16) | P.Active[0], (P.Active[3] << 16) | P.Active[2]);
             if ((na.x != act.x) | (na.y != act.y)) L.act[s] = na;
         } else {
+            ShadeMark(SM_COMPLETED);
             float4* A = &F.accum[(size_t)y * F.width + x];
             float4 Val = make_float4(P.Sample.x, P.Sample.y, P.Sample.z, 1.0f);
             if (Pm.render_flags & PT_RENDER_FLAG_ACCUMULATE) {
@@ -1641,8 +1388,7 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
     // updated by the wave's first lane (no atomics: a wave owns its word).
     uint64_t cm = __ballot(completed);
     if ((threadIdx.x & 63u) == 0) L.done[(base | threadIdx.x) >> 6] += (uint32_t)__popcll(cm);
-    if (L.gsort) GlobalSortStoreRay(S, L, s, valid, O, V);
-    else TileOrderStoreRay(L, s, valid, O, V, p16 >> 8);
+    TileOrderStoreRay(L, s, valid, O, V, p16 >> 8);
 }
 
 template <uint32_t MATS>
@@ -1651,7 +1397,9 @@ __global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void shade_kernel(dscen
 {
     // Tiles in extend's longest-first order too: tiles with long traversals
     // also shade more hits (C5 shade -3 %).
-    ShadeTile<MATS>(S, L, F, Pm, L.order ? L.order[blockIdx.x] : L.tile_base + blockIdx.x);
+    ShadeStatsBegin();
+    ShadeTile<MATS>(S, L, F, Pm, L.order ? L.order[blockIdx.x] : blockIdx.x);
+    ShadeStatsEnd();
 }
 
 // One round (extend + shade) of a tile per block, for partitions whose tiles
@@ -1665,7 +1413,7 @@ __global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void round_kernel(
     dscene S, dslots L, dframe F, dparams Pm)
 {
     __shared__ E smem[CAP * 256];
-    const uint32_t tile = L.order ? L.order[blockIdx.x] : L.tile_base + blockIdx.x;
+    const uint32_t tile = L.order ? L.order[blockIdx.x] : blockIdx.x;
     ExtendTile<ray_source_slots, false, CAP, E>(S, ray_source_slots{L, F}, L.n, nullptr, 0, smem, tile,
                                                  L.order != nullptr);
     // The tile's hits and outcome masks (global, written by all four waves)
@@ -1692,7 +1440,7 @@ __global__ __launch_bounds__(256, PT_ROUNDS_MINW ? PT_ROUNDS_MINW : ShadeMinWave
     dscene S, dslots L, dframe F, dparams Pm)
 {
     __shared__ E smem[CAP * 256];
-    const uint32_t tile = L.order ? L.order[blockIdx.x] : L.tile_base + blockIdx.x;
+    const uint32_t tile = L.order ? L.order[blockIdx.x] : blockIdx.x;
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     dparams P = Pm;
     for (uint32_t i = 0; i < Pm.rounds; i++) {
@@ -1760,80 +1508,66 @@ hipError_t pt_launch_raygen(const ptd::dscene& S, const ptd::dslots& L, const pt
     return hipGetLastError();
 }
 
-// Occupancy variants of the extend kernel: {min waves per SIMD, LDS stack
-// entries per thread}.  Selected with PT_EXTEND_VARIANT (default 0); stack
-// entries beyond the LDS capacity spill to a global buffer.
-// Scenes whose stack entries all fit 16 bits (dscene::stack16) run the same
-// variant with a u16 stack.
-#define PT_EXTEND_VARIANTS(X) X(0, 5, 20) X(1, 4, 24) X(2, 6, 16) X(3, 4, 32) X(4, 8, 16) X(5, 8, 12)
+// Extend occupancy: min waves per SIMD and LDS stack entries per thread
+// (entries beyond the LDS capacity spill to a global buffer).  Compile-time
+// only (tools/build_variant.py -DPT_EXTEND_MINW=.. -DPT_EXTEND_CAP=..); the
+// round kernels share PT_EXTEND_CAP.  Measured alternatives (4/24, 6/16,
+// 4/32, 8/16, 8/12) were all slower on C3.  Scenes whose
+// stack entries all fit 16 bits (dscene::stack16) run a u16 stack.
+#ifndef PT_EXTEND_MINW
+#define PT_EXTEND_MINW 5
+#endif
+#ifndef PT_EXTEND_CAP
+#define PT_EXTEND_CAP 20
+#endif
 
-int pt_extend_variant()
-{
-    static int v = []() {
-        const char* e = getenv("PT_EXTEND_VARIANT");
-        int x = e ? atoi(e) : 0;
-        return (x >= 0 && x <= 5) ? x : 0;
-    }();
-    return v;
-}
+uint32_t pt_extend_stack_cap() { return PT_EXTEND_CAP; }
 
-uint32_t pt_extend_stack_cap()
-{
-    switch (pt_extend_variant()) {
-#define X(id, w, cap) case id: return cap;
-        PT_EXTEND_VARIANTS(X)
-#undef X
-    }
-    return 20;
-}
-
-template <class Src, int W, int CAP, class E>
+template <class Src, class E>
 static void LaunchExtendE(const ptd::dscene& S, const Src& src, uint32_t n, uint32_t blocks, uint32_t* spill,
-                          uint32_t pad, hipStream_t st)
+                          hipStream_t st)
 {
     if (spill)
-        hipLaunchKernelGGL((ptd::extend_kernel<Src, true, W, CAP, E>), dim3(blocks), dim3(256), pad, st, S, src, n,
-                           spill, n);
+        hipLaunchKernelGGL((ptd::extend_kernel<Src, true, PT_EXTEND_MINW, PT_EXTEND_CAP, E>), dim3(blocks), dim3(256),
+                           0, st, S, src, n, spill, n);
     else
-        hipLaunchKernelGGL((ptd::extend_kernel<Src, false, W, CAP, E>), dim3(blocks), dim3(256), pad, st, S, src, n,
-                           spill, n);
+        hipLaunchKernelGGL((ptd::extend_kernel<Src, false, PT_EXTEND_MINW, PT_EXTEND_CAP, E>), dim3(blocks),
+                           dim3(256), 0, st, S, src, n, spill, n);
 }
 
 // n: rays (the spill stride and the bound of the ray index); blocks: the
-// launch's 256-ray blocks (a run group's tiles for the slot renderer).
+// launch's 256-ray blocks (the renderer's tiles).
 template <class Src>
 static hipError_t LaunchExtend(const ptd::dscene& S, const Src& src, uint32_t n, uint32_t blocks, uint32_t* spill,
                                hipStream_t st)
 {
     if (n == 0 || blocks == 0) return hipSuccess;
-    // PT_EXTEND_LDS_PAD: extra (unused) dynamic LDS per block, an occupancy cap
-    // for experiments (e.g. 12288 -> 5 blocks per CU).
-    static const uint32_t pad = []() {
-        const char* e = getenv("PT_EXTEND_LDS_PAD");
-        return e ? (uint32_t)atoi(e) : 0u;
-    }();
-    switch (pt_extend_variant()) {
-#define X(id, w, cap)                                                                                           \
-    case id:                                                                                                   \
-        if (S.stack16) LaunchExtendE<Src, w, cap, uint16_t>(S, src, n, blocks, spill, pad, st);                 \
-        else LaunchExtendE<Src, w, cap, uint32_t>(S, src, n, blocks, spill, pad, st);                           \
-        break;
-        PT_EXTEND_VARIANTS(X)
-#undef X
-    }
+    if (S.stack16) LaunchExtendE<Src, uint16_t>(S, src, n, blocks, spill, st);
+    else LaunchExtendE<Src, uint32_t>(S, src, n, blocks, spill, st);
     return hipGetLastError();
 }
 
-template <int CAP, class E, class Src>
-static void LaunchExtendStats(const ptd::dscene& S, const Src& src, uint32_t n, uint32_t* spill,
-                              unsigned long long* out, uint32_t* steps, hipStream_t st)
+template <class Src>
+static hipError_t LaunchExtendStats(const ptd::dscene& S, const Src& src, uint32_t n, uint32_t* spill,
+                                    unsigned long long* out, uint32_t* steps, hipStream_t st)
 {
-    if (spill)
-        hipLaunchKernelGGL((ptd::extend_stats_kernel<Src, true, CAP, E>), dim3(Blocks(n)), dim3(256),
-                           0, st, S, src, n, spill, n, out, steps);
-    else
-        hipLaunchKernelGGL((ptd::extend_stats_kernel<Src, false, CAP, E>), dim3(Blocks(n)),
-                           dim3(256), 0, st, S, src, n, spill, n, out, steps);
+    // The same LDS stack capacity and entry width as the render kernel.
+    if (S.stack16) {
+        if (spill)
+            hipLaunchKernelGGL((ptd::extend_stats_kernel<Src, true, PT_EXTEND_CAP, uint16_t>), dim3(Blocks(n)),
+                               dim3(256), 0, st, S, src, n, spill, n, out, steps);
+        else
+            hipLaunchKernelGGL((ptd::extend_stats_kernel<Src, false, PT_EXTEND_CAP, uint16_t>), dim3(Blocks(n)),
+                               dim3(256), 0, st, S, src, n, spill, n, out, steps);
+    } else {
+        if (spill)
+            hipLaunchKernelGGL((ptd::extend_stats_kernel<Src, true, PT_EXTEND_CAP, uint32_t>), dim3(Blocks(n)),
+                               dim3(256), 0, st, S, src, n, spill, n, out, steps);
+        else
+            hipLaunchKernelGGL((ptd::extend_stats_kernel<Src, false, PT_EXTEND_CAP, uint32_t>), dim3(Blocks(n)),
+                               dim3(256), 0, st, S, src, n, spill, n, out, steps);
+    }
+    return hipGetLastError();
 }
 
 hipError_t pt_launch_trace_rays_stats(const ptd::dscene& S, uint32_t n, const float* origins, const uint32_t* vel,
@@ -1841,50 +1575,14 @@ hipError_t pt_launch_trace_rays_stats(const ptd::dscene& S, uint32_t n, const fl
                                       unsigned long long* out, uint32_t* steps, hipStream_t st)
 {
     if (n == 0) return hipSuccess;
-    ptd::ray_source_arrays src{origins, vel, dur, hit, hc};
-    switch (pt_extend_variant()) {
-#define X(id, w, cap)                                                                                           \
-    case id:                                                                                                   \
-        if (S.stack16) LaunchExtendStats<cap, uint16_t>(S, src, n, spill, out, steps, st);                      \
-        else LaunchExtendStats<cap, uint32_t>(S, src, n, spill, out, steps, st);                                \
-        break;
-        PT_EXTEND_VARIANTS(X)
-#undef X
-    }
-    return hipGetLastError();
+    return LaunchExtendStats(S, ptd::ray_source_arrays{origins, vel, dur, hit, hc}, n, spill, out, steps, st);
 }
 
 hipError_t pt_launch_extend_stats(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* spill,
                                   unsigned long long* out, uint32_t* steps, hipStream_t st)
 {
     if (L.n == 0) return hipSuccess;
-    ptd::ray_source_slots src{L, F};
-    ptd::ray_source_slot_rays gsrc{L, F};
-    // The same LDS stack capacity and entry width as the render kernel.
-    switch (pt_extend_variant()) {
-#define X(id, w, cap)                                                                                           \
-    case id:                                                                                                   \
-        if (L.gsort) {                                                                                         \
-            if (S.stack16) LaunchExtendStats<cap, uint16_t>(S, gsrc, L.n, spill, out, steps, st);              \
-            else LaunchExtendStats<cap, uint32_t>(S, gsrc, L.n, spill, out, steps, st);                        \
-        } else if (S.stack16) LaunchExtendStats<cap, uint16_t>(S, src, L.n, spill, out, steps, st);           \
-        else LaunchExtendStats<cap, uint32_t>(S, src, L.n, spill, out, steps, st);                              \
-        break;
-        PT_EXTEND_VARIANTS(X)
-#undef X
-    }
-    return hipGetLastError();
-}
-
-hipError_t pt_launch_gsort(const ptd::dslots& L, const ptd::dframe& F, uint32_t* cursor, hipStream_t st)
-{
-    if (L.n == 0) return hipSuccess;
-    static_assert(PT_GS_BINS % ptd::GS_THREADS == 0, "scan: whole bins per thread");
-    const uint32_t chunks = (L.n + ptd::GS_CHUNK - 1) / ptd::GS_CHUNK;
-    hipLaunchKernelGGL(ptd::gsort_count_kernel, dim3(chunks), dim3(ptd::GS_THREADS), 0, st, L, F);
-    hipLaunchKernelGGL(ptd::gsort_scan_kernel, dim3(1), dim3(ptd::GS_THREADS), 0, st, L, cursor);
-    hipLaunchKernelGGL(ptd::gsort_scatter_kernel, dim3(chunks), dim3(ptd::GS_THREADS), 0, st, L, F, cursor);
-    return hipGetLastError();
+    return LaunchExtendStats(S, ptd::ray_source_slots{L, F}, L.n, spill, out, steps, st);
 }
 
 hipError_t pt_launch_vertex_decode(const uint2* v, uint32_t n, float4* attr, float* vv, hipStream_t st)
@@ -1897,8 +1595,7 @@ hipError_t pt_launch_vertex_decode(const uint2* v, uint32_t n, float4* attr, flo
 hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st)
 {
     if (!L.order || L.tile_count == 0) return hipSuccess;
-    hipLaunchKernelGGL(ptd::tile_order_kernel, dim3(1), dim3(1024), 0, st, L.tilecost, L.order, L.tile_base,
-                       L.tile_count);
+    hipLaunchKernelGGL(ptd::tile_order_kernel, dim3(1), dim3(1024), 0, st, L.tilecost, L.order, L.tile_count);
     return hipGetLastError();
 }
 
@@ -1924,7 +1621,6 @@ hipError_t pt_launch_zero_unowned(float4* accum, uint32_t width, uint32_t height
 hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* spill,
                             hipStream_t st)
 {
-    if (L.gsort) return LaunchExtend(S, ptd::ray_source_sorted{L, F}, L.n, L.tile_count, spill, st);
     return LaunchExtend(S, ptd::ray_source_slots{L, F}, L.n, L.tile_count, spill, st);
 }
 
@@ -1933,7 +1629,7 @@ hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const pt
 // width.  Capacity = the tiles the GPU holds at once (blocks per CU at the
 // kernel's occupancy x CUs); a larger partition runs extend + shade.
 template <uint32_t MATS, class E>
-static const void* RoundKernel() { return reinterpret_cast<const void*>(&ptd::round_kernel<MATS, 20, E>); }
+static const void* RoundKernel() { return reinterpret_cast<const void*>(&ptd::round_kernel<MATS, PT_EXTEND_CAP, E>); }
 
 static const void* RoundKernelFor(uint32_t mats, bool stack16)
 {
@@ -1951,7 +1647,6 @@ static const void* RoundKernelFor(uint32_t mats, bool stack16)
 
 uint32_t pt_round_capacity(uint32_t scene_mats, bool stack16, uint32_t cu_count)
 {
-    if (pt_extend_variant() != 0) return 0;   // round_kernel has the default variant's 20-entry stack
     // Blocks per CU of the round kernel instantiation, cached per (device,
     // shade mask, stack entry width); renderers may be created from several
     // host threads and on several devices.
@@ -1976,7 +1671,7 @@ hipError_t pt_launch_round(const ptd::dscene& S, const ptd::dslots& L, const ptd
                            uint32_t scene_mats, hipStream_t st)
 {
     if (L.n == 0 || L.tile_count == 0) return hipSuccess;
-    if (L.spill || pt_extend_variant() != 0) return hipErrorNotSupported;
+    if (L.spill) return hipErrorNotSupported;
     const void* k = RoundKernelFor(scene_mats, S.stack16 != 0);
     void* args[] = {const_cast<ptd::dscene*>(&S), const_cast<ptd::dslots*>(&L), const_cast<ptd::dframe*>(&F),
                     const_cast<ptd::dparams*>(&P)};
@@ -1984,7 +1679,7 @@ hipError_t pt_launch_round(const ptd::dscene& S, const ptd::dslots& L, const ptd
 }
 
 template <uint32_t MATS, class E>
-static const void* RoundsKernel() { return reinterpret_cast<const void*>(&ptd::rounds_kernel<MATS, 20, E>); }
+static const void* RoundsKernel() { return reinterpret_cast<const void*>(&ptd::rounds_kernel<MATS, PT_EXTEND_CAP, E>); }
 
 static const void* RoundsKernelFor(uint32_t mats, bool stack16)
 {
@@ -2000,11 +1695,10 @@ static const void* RoundsKernelFor(uint32_t mats, bool stack16)
     }
 }
 
-// Round batches need the round kernel's conditions: no spilled stack, the
-// default extend variant, tile order (not the global sort).
+// Round batches need the round kernel's condition: no spilled stack.
 bool pt_rounds_available(const ptd::dslots& L)
 {
-    return !L.spill && !L.gsort && pt_extend_variant() == 0;
+    return !L.spill;
 }
 
 hipError_t pt_launch_rounds(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
@@ -2050,6 +1744,22 @@ hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd
     }
     return hipGetLastError();
 }
+
+#if PT_SHADE_STATS
+// Experiment build only (tools/shade_stats.py): the launch-summed shade
+// branch counters {waves, lanes} x SM_COUNT; reset clears them.
+extern "C" int ptShadeStatsRead(unsigned long long* out, int reset)
+{
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(ptd::g_shade_stats), sizeof(ptd::g_shade_stats)) != hipSuccess)
+        return -1;
+    if (reset) {
+        unsigned long long z[2 * 32] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(ptd::g_shade_stats), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return (int)ptd::SM_COUNT;
+}
+#endif
 
 hipError_t pt_launch_rcp_check(unsigned long long* mismatches, hipStream_t st)
 {

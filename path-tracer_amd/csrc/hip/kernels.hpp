@@ -6,13 +6,6 @@
 #include "../../../include/pt_packed.h"
 #include "../../../include/pt_api.h"
 
-// Traversal-stack entries kept in LDS per thread (TLAS + BLAS combined);
-// deeper entries go to a per-slot global spill area (only allocated when the
-// scene's BVH depths need it).
-#ifndef PT_LDS_STACK
-#define PT_LDS_STACK 24
-#endif
-
 namespace ptd {
 
 struct dscene;
@@ -38,22 +31,8 @@ struct dslots {
     uint32_t* order;    // extend's block -> tile map (longest previous extend first), or null
     uint32_t* done;     // per wave of 64 slots: paths completed by shade since the last Reset (ptGetStats)
     uint32_t* spill;    // traversal stack spill: (needed - LDS capacity) rows x n
-    // Global ray sort (gsort != 0, kernels.hip "Global ray sort"): extend
-    // traces the rays in key order over the whole frame instead of tile by
-    // tile.  `ray` is then indexed by slot, and:
-    uint32_t* perm;     // per position: the slot whose ray extend traces there
-    uint32_t* nvalid;   // positions [0, *nvalid) hold rays (slots inside the image)
-    uint16_t* key;      // per slot: sort key of its current ray (RayKey, written by raygen / shade)
-    uint32_t* hist;     // per key bin: the frame's count (sort pass; cleared by the scan)
-    uint8_t* cls;       // per position: the traced ray's ShadeOrder outcome class
-    uint2* binprev;     // per key bin: {first position, count} in the last extend
-    uint32_t gsort;
-    uint32_t gcost;     // bins in descending order of their previous-round cost (else key order)
     uint32_t n;
-    // The launch's tile range (a run group, runtime.hip): tiles
-    // [tile_base, tile_base + tile_count); `order` then points at the group's
-    // segment of the block -> tile map.
-    uint32_t tile_base, tile_count;
+    uint32_t tile_count;    // n / 256: one block per tile
 };
 
 struct dframe {
@@ -105,10 +84,6 @@ hipError_t pt_launch_resolve(const float4* accum, uint32_t n, float brightness, 
                              uint32_t* out8, hipStream_t st);
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
                            uint32_t scene_mats, hipStream_t st);
-// Global ray sort before an extend: key counts (hist), their exclusive prefix
-// sums (cursor, hist cleared), then every position's slot (perm).  PT_GS_BINS key bins + one for slots outside the image.
-constexpr uint32_t PT_GS_BINS = 4096;
-hipError_t pt_launch_gsort(const ptd::dslots& L, const ptd::dframe& F, uint32_t* cursor, hipStream_t st);
 hipError_t pt_launch_vertex_decode(const uint2* v, uint32_t n, float4* attr, float* vv, hipStream_t st);
 hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st);
 // Fused round (extend + shade per tile in one launch, round_kernel): the
@@ -140,5 +115,4 @@ hipError_t pt_launch_trace_rays(const ptd::dscene& S, uint32_t n, const float* o
                                 hipStream_t st);
 hipError_t pt_launch_finalize(const ptd::dscene& S, uint32_t n, const float4* hit, const float2* hc, float4* rec,
                               float2* uv, hipStream_t st);
-int pt_extend_variant();
 uint32_t pt_extend_stack_cap();

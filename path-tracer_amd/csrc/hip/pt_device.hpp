@@ -5,7 +5,7 @@
 // src/core/spectrum.glsl.inc, src/integrator/basic_scatter.glsl) under the
 // numerics convention of include/pt_fp.h.  Scene data is read through
 // 16-byte vector loads; the traversal stack lives in LDS with a global
-// spill area for depth beyond PT_LDS_STACK (see extend kernel).
+// spill area for depth beyond its LDS capacity (PT_EXTEND_CAP, kernels.hip).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -26,6 +26,7 @@ struct dscene {
     const pt_packed_texture* textures;
     const uint32_t* material;
     const pt_packed_shape* shapes;
+    const uint8_t* shape_uv;       // per shape: its material samples a texture (shade needs the hit's UV)
     const float4* shape_nodes;     // 2 x float4 per node
     const float4* mesh_faces;      // 3 x float4 per face: {Position0, Edge1, Edge2}, .w = vertex indices
     const uint2* mesh_vertices;
@@ -447,10 +448,14 @@ PT_DEV size_t AtlasIndex(const dscene& S, uint32_t Layer, uint32_t X, uint32_t Y
 
 PT_DEV float4 Texel(const dscene& S, uint32_t Layer, int X, int Y)
 {
-    int W = (int)S.atlas_w, H = (int)S.atlas_h;
-    X %= W; if (X < 0) X += W;
-    Y %= H; if (Y < 0) Y += H;
     if (S.atlas_layers == 0) return make_float4(0, 0, 0, 0);
+    int W = (int)S.atlas_w, H = (int)S.atlas_h;
+    // REPEAT wrap, X mod W in [0, W).  A coordinate already in range is its
+    // own remainder, so only the footprints crossing a texture's edge (I0 =
+    // -1 or I0 + 1 = W) take the integer remainder -- about 30 VALU per
+    // coordinate, 8 per bilinear sample when it ran unconditionally.
+    if ((uint32_t)X >= (uint32_t)W) { X %= W; if (X < 0) X += W; }
+    if ((uint32_t)Y >= (uint32_t)H) { Y %= H; if (Y < 0) Y += H; }
     if (Layer >= S.atlas_layers) Layer = S.atlas_layers - 1;
     return S.atlas[AtlasIndex(S, Layer, (uint32_t)X, (uint32_t)Y)];
 }

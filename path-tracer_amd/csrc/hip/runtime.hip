@@ -13,12 +13,14 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -74,7 +76,7 @@ struct dbuf {
     }
 };
 
-struct event_pair { hipEvent_t a, b; int kernel; hipStream_t stream; };
+struct event_pair { hipEvent_t a, b; int kernel; uint32_t rounds; hipStream_t stream; };
 
 }  // namespace
 
@@ -87,7 +89,14 @@ struct pt_device {
     uint64_t run_tick = 0;
     std::vector<event_pair> pending;
     std::vector<event_pair> free_events;
+    // Live RCCL communicators on this device: while one exists, the blocking
+    // calls wait for the stream by polling it together with RCCL's
+    // asynchronous error state and a deadline (DeviceWait), so a collective
+    // whose peer died returns an error instead of hanging.
+    std::vector<pt_comm*> comms;
+    bool comm_failed = false;      // a communicator was aborted: waits keep a short deadline
     uint64_t launches[PT_KERNEL_COUNT] = {};
+    uint64_t rounds[PT_KERNEL_COUNT] = {};    // rounds the timed launches covered (a batch: its rounds)
     double total_ms[PT_KERNEL_COUNT] = {};
 };
 
@@ -97,6 +106,7 @@ struct pt_scene {
     dbuf<pt_packed_texture> textures;
     dbuf<uint32_t> material;
     dbuf<pt_packed_shape> shapes;
+    dbuf<uint8_t> shape_uv;              // per shape: its material reads texture coordinates
     dbuf<pt_packed_shape_node> shape_nodes;
     dbuf<pt_packed_mesh_face> faces;
     dbuf<pt_packed_mesh_vertex> vertices;
@@ -109,6 +119,8 @@ struct pt_scene {
     uint32_t camera_count = 0;
     uint32_t stack_needed = 0;   // max traversal stack entries (TLAS + BLAS)
     uint32_t mats = PT_MATS_ALL; // material types referenced by shapes (shade specialisation)
+    uint32_t stack_format = PT_STACK_FORMAT_AUTO;   // ptSetSceneStackFormat (applied at the next update)
+    uint32_t hit_record = PT_HIT_RECORD_AUTO;       // ptSetSceneHitRecordForm (applied at the next update)
     bool valid = false;
 };
 
@@ -135,21 +147,6 @@ struct pt_preview {
 };
 
 namespace {
-int FusedDefault()
-{
-    const char* e = getenv("PT_ROUND_FUSED");
-    return e ? atoi(e) : 1;
-}
-
-// Round-batch mode (ptSetBasicRendererRoundBatch): the PT_ROUND_BATCH
-// environment variable, else 0 (automatic).
-uint32_t RoundBatchDefault()
-{
-    const char* e = getenv("PT_ROUND_BATCH");
-    int x = e ? atoi(e) : 0;
-    return (uint32_t)std::max(0, x);
-}
-
 // Automatic mode's batch for a renderer whose tiles all fit on the GPU at
 // once (RoundFused's condition): one launch per AUTO_BATCH rounds.
 constexpr uint32_t AUTO_BATCH = 16;
@@ -173,24 +170,9 @@ struct pt_basic_renderer {
     dbuf<uint32_t> tilecost, order;     // longest-first tile order (extend -> tile_order -> extend)
     uint64_t order_tick = 0;            // rounds since creation (tile-order re-sort period)
     dbuf<uint32_t> done;                // per wave: completed paths since the last Reset (ptGetStats)
-    // Global ray sort (PT_GLOBAL_SORT, kernels.hip): per-position slot, per-slot
-    // position and key, key-bin counts and cursors, per-position outcome class.
-    dbuf<uint32_t> perm, nvalid, hist, cursor;
-    dbuf<uint16_t> key;
-    dbuf<uint8_t> cls;
-    dbuf<uint2> binprev;
-    // Run groups: the tiles split into `groups` contiguous ranges, each
-    // advanced round by round on its own stream, so a group's next round
-    // starts while another group's extend is still draining its longest
-    // tiles (a partition too small to fill the GPU: strong scaling).
-    static constexpr uint32_t MAX_GROUPS = 4;
-    uint32_t groups = 1;
-    int fused = FusedDefault();         // fused rounds mode (ptSetBasicRendererFusedRounds)
+    int fused = 1;                      // fused rounds mode (ptSetBasicRendererFusedRounds)
     int openpbr = 0;                    // shade OpenPBR materials (ptSetBasicRendererOpenPBR)
-    uint32_t round_batch = RoundBatchDefault();   // rounds per launch of consecutive Run(1) rounds
-    hipStream_t gstream[MAX_GROUPS] = {};
-    hipEvent_t gevent[MAX_GROUPS] = {};
-    hipEvent_t fork = nullptr;
+    uint32_t round_batch = 0;           // rounds per launch of consecutive Run(1) rounds (0: automatic)
     uint64_t pixels = 0;                // image pixels owned (valid slots)
     uint64_t rays = 0;                  // rays traced since the last Reset
     dbuf<uint32_t> spill;
@@ -200,11 +182,78 @@ struct pt_comm {
     pt_device* dev = nullptr;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    double timeout_s = 600.0;     // ptCommSetTimeout
+    bool aborted = false;
+    int* flag = nullptr;          // device word of the collective argument check (CommAgree)
 };
 
 namespace {
 
-int BeginTimed(pt_device* dev, int kernel, event_pair& ep, bool sampled = true, hipStream_t stream = nullptr)
+// Aborts every communicator of the device (ncclCommAbort: RCCL stops their
+// kernels) after a failed or overdue collective.
+void AbortComms(pt_device* dev)
+{
+    for (pt_comm* c : dev->comms) {
+        if (c->comm) (void)ncclCommAbort(c->comm);
+        c->comm = nullptr;
+        c->aborted = true;
+    }
+    dev->comms.clear();
+    dev->comm_failed = true;
+}
+
+// Waits until the device stream is idle.  With no communicator: one
+// hipStreamSynchronize.  With live communicators: polls the stream, each
+// communicator's asynchronous error (ncclCommGetAsyncError) and the shortest
+// communicator deadline; on an RCCL error or at the deadline every
+// communicator is aborted and PT_ERROR_COMM_ABORTED / PT_ERROR_TIMEOUT
+// returned.  After an abort, waits give up after 10 s (PT_ERROR_TIMEOUT).
+int DeviceWait(pt_device* dev)
+{
+    if (dev->comms.empty() && !dev->comm_failed) {
+        PT_HIP(hipStreamSynchronize(dev->stream));
+        return 0;
+    }
+    double limit = dev->comm_failed ? 10.0 : 1e30;
+    for (pt_comm* c : dev->comms) limit = std::min(limit, c->timeout_s);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0;; spin++) {
+        hipError_t q = hipStreamQuery(dev->stream);
+        if (q == hipSuccess) {
+            if (dev->comms.empty()) dev->comm_failed = false;   // drained since the abort
+            return 0;
+        }
+        if (q != hipErrorNotReady) {
+            SetError("device stream: %s", hipGetErrorString(q));
+            return (int)q;
+        }
+        for (pt_comm* c : dev->comms) {
+            ncclResult_t st = ncclSuccess;
+            ncclResult_t r = ncclCommGetAsyncError(c->comm, &st);
+            if (r != ncclSuccess || (st != ncclSuccess && st != ncclInProgress)) {
+                SetError("RCCL communicator (rank %d of %d) failed: %s; communicators aborted", c->rank, c->nranks,
+                         ncclGetErrorString(r != ncclSuccess ? r : st));
+                AbortComms(dev);
+                return PT_ERROR_COMM_ABORTED;
+            }
+        }
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (el > limit) {
+            SetError("device stream not idle after %.1f s with a live communicator (a peer rank failed or stalled); "
+                     "communicators aborted", el);
+            AbortComms(dev);
+            return PT_ERROR_TIMEOUT;
+        }
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
+#define PT_WAIT(dev)                                    \
+    do {                                                \
+        if (int w_ = DeviceWait(dev)) return w_;        \
+    } while (0)
+
+int BeginTimed(pt_device* dev, int kernel, event_pair& ep, bool sampled = true, uint32_t rounds = 1)
 {
     ep.kernel = -1;
     if (!dev->profiling || !sampled) return 0;
@@ -214,7 +263,8 @@ int BeginTimed(pt_device* dev, int kernel, event_pair& ep, bool sampled = true, 
         PT_HIP(hipEventCreate(&ep.b));
     }
     ep.kernel = kernel;
-    ep.stream = stream ? stream : dev->stream;
+    ep.rounds = rounds;
+    ep.stream = dev->stream;
     PT_HIP(hipEventRecord(ep.a, ep.stream));
     return 0;
 }
@@ -230,11 +280,12 @@ int EndTimed(pt_device* dev, event_pair& ep)
 int CollectTimes(pt_device* dev)
 {
     if (dev->pending.empty()) return 0;
-    PT_HIP(hipStreamSynchronize(dev->stream));
+    PT_WAIT(dev);
     for (event_pair& ep : dev->pending) {
         float ms = 0;
         PT_HIP(hipEventElapsedTime(&ms, ep.a, ep.b));
         dev->launches[ep.kernel] += 1;
+        dev->rounds[ep.kernel] += ep.rounds;
         dev->total_ms[ep.kernel] += ms;
         dev->free_events.push_back(ep);
     }
@@ -435,7 +486,7 @@ void ptDestroyDevice(pt_device* d)
 {
     if (!d) return;
     (void)hipSetDevice(d->id);
-    (void)hipStreamSynchronize(d->stream);
+    (void)DeviceWait(d);
     for (auto& ep : d->pending) { (void)hipEventDestroy(ep.a); (void)hipEventDestroy(ep.b); }
     for (auto& ep : d->free_events) { (void)hipEventDestroy(ep.a); (void)hipEventDestroy(ep.b); }
     (void)hipStreamDestroy(d->stream);
@@ -446,7 +497,7 @@ int ptSynchronize(pt_device* d)
 {
     if (!d) { SetError("null device"); return -1; }
     PT_HIP(hipSetDevice(d->id));
-    PT_HIP(hipStreamSynchronize(d->stream));
+    PT_WAIT(d);
     return 0;
 }
 
@@ -462,9 +513,23 @@ void ptDestroyScene(pt_device* d, pt_scene* s)
 {
     if (!s) return;
     if (d) (void)hipSetDevice(d->id);
-    s->textures.release(); s->material.release(); s->shapes.release(); s->shape_nodes.release();
+    s->textures.release(); s->material.release(); s->shapes.release(); s->shape_uv.release(); s->shape_nodes.release();
     s->faces.release(); s->vertices.release(); s->vertex_attr.release(); s->vertex_v.release(); s->mesh_nodes.release(); s->cameras.release(); s->atlas.release();
     delete s;
+}
+
+int ptSetSceneStackFormat(pt_scene* s, uint32_t format)
+{
+    if (!s || format > PT_STACK_FORMAT_NODE_INDEX) { SetError("ptSetSceneStackFormat: bad argument"); return -1; }
+    s->stack_format = format;
+    return 0;
+}
+
+int ptSetSceneHitRecordForm(pt_scene* s, uint32_t form)
+{
+    if (!s || form > PT_HIT_RECORD_FACE_INDEX) { SetError("ptSetSceneHitRecordForm: bad argument"); return -1; }
+    s->hit_record = form;
+    return 0;
 }
 
 // UpdateVulkanScene (scene.cpp:1692-2006): synchronous upload of the packs.
@@ -488,11 +553,9 @@ static bool FastDivBoxes(const pt_scene_packs* p)
 
 // Whether every BLAS node's index words fit one packed stack entry
 // (PackBlasEntry): leaves with <= 31 faces starting below 2^26, child-pair
-// indices below 2^31.  PT_BLAS_WORDS=0 forces the index form (A/B testing).
+// indices below 2^31.
 static bool BlasWordsPackable(const pt_scene_packs* p)
 {
-    const char* e = getenv("PT_BLAS_WORDS");
-    if (e && atoi(e) == 0) return false;
     for (uint32_t i = 0; i < p->mesh_node_count; i++) {
         const pt_packed_mesh_node& n = p->mesh_nodes[i];
         if (n.FaceEndIndex > 0) {
@@ -510,11 +573,8 @@ static bool BlasWordsPackable(const pt_scene_packs* p)
 // first face index, or 0 if some entry does not fit.  Internal entries are
 // child-pair indices < 2^15; a leaf needs first < 2^F and count < 2^(15-F)
 // for one F; TLAS entries are node indices < 2^16 (ValidatePacks).
-// PT_STACK16=0 disables it.
 static uint32_t BlasWords16FirstBits(const pt_scene_packs* p)
 {
-    const char* e = getenv("PT_STACK16");
-    if (e && atoi(e) == 0) return 0;
     if (p->shape_node_count > 65536) return 0;
     uint32_t max_first = 0, max_count = 0;
     for (uint32_t i = 0; i < p->mesh_node_count; i++) {
@@ -530,6 +590,27 @@ static uint32_t BlasWords16FirstBits(const pt_scene_packs* p)
     for (uint32_t F = 1; F < 15; F++)
         if (max_first < (1u << F) && max_count < (1u << (15 - F))) return F;
     return 0;
+}
+
+// Whether shading a hit on material m reads the hit's texture coordinates:
+// some texture index among the fields its BSDF reads (MaterialOk's list, and
+// OpenPBR's base colour and specular roughness textures) is set.  Hits on
+// other materials skip computing their UV (HitAttributesV).
+static bool MaterialReadsUV(const pt_scene_packs* p, uint32_t m)
+{
+    const uint32_t* A = p->material_data + 32 * (size_t)m;
+    auto tx = [&](uint32_t w) { return A[w] != PT_TEXTURE_INDEX_NONE; };
+    switch (A[0]) {
+        case PT_MATERIAL_TYPE_BASIC_DIFFUSE: return tx(PT_BASIC_DIFFUSE_BASE_SPECTRUM + 3);
+        case PT_MATERIAL_TYPE_BASIC_METAL:
+            return tx(PT_BASIC_METAL_BASE_SPECTRUM + 3) || tx(PT_BASIC_METAL_SPECULAR_SPECTRUM + 3) ||
+                   tx(PT_BASIC_METAL_ROUGHNESS + 1) || tx(PT_BASIC_METAL_ROUGHNESS_ANISOTROPY + 1);
+        case PT_MATERIAL_TYPE_BASIC_TRANSLUCENT:
+            return tx(PT_BASIC_TRANSLUCENT_ROUGHNESS + 1) || tx(PT_BASIC_TRANSLUCENT_ROUGHNESS_ANISOTROPY + 1);
+        case PT_MATERIAL_TYPE_OPENPBR:
+            return tx(PT_OPENPBR_BASE_SPECTRUM_TEXTURE_INDEX) || tx(PT_OPENPBR_SPECULAR_ROUGHNESS_TEXTURE_INDEX);
+        default: return false;   // not shaded: the path ends
+    }
 }
 
 // Material types reachable by a hit (every shape's material) plus whether any
@@ -554,7 +635,7 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     uint32_t need = 0;
     if (ValidatePacks(p, &need) != 0) { s->valid = false; return -1; }
     PT_HIP(hipSetDevice(d->id));
-    PT_HIP(hipStreamSynchronize(d->stream));   // like vkDeviceWaitIdle (scene.cpp:1704)
+    PT_WAIT(d);   // like vkDeviceWaitIdle (scene.cpp:1704)
     bool first = !s->valid;
     if (first || (dirty & PT_SCENE_DIRTY_TEXTURES)) {
         PT_HIP(s->textures.upload(p->textures, p->texture_count));
@@ -569,7 +650,7 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
             PT_HIP(s->atlas.alloc(atlas_floats));
             PT_HIP(pt_launch_atlas_tile(reinterpret_cast<const float4*>(stage.ptr), reinterpret_cast<float4*>(s->atlas.ptr),
                                         p->atlas_width, p->atlas_height, p->atlas_layer_count, d->stream));
-            PT_HIP(hipStreamSynchronize(d->stream));
+            PT_WAIT(d);
         } else {
             PT_HIP(s->atlas.upload(p->atlas, p->atlas ? atlas_floats : 0));
         }
@@ -578,6 +659,11 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     if (first || (dirty & PT_SCENE_DIRTY_SHAPES)) {
         PT_HIP(s->shapes.upload(p->shapes, p->shape_count));
         PT_HIP(s->shape_nodes.upload(p->shape_nodes, p->shape_node_count));
+    }
+    if (first || (dirty & (PT_SCENE_DIRTY_SHAPES | PT_SCENE_DIRTY_MATERIALS))) {
+        std::vector<uint8_t> uv(p->shape_count);
+        for (uint32_t i = 0; i < p->shape_count; i++) uv[i] = MaterialReadsUV(p, p->shapes[i].MaterialIndex) ? 1 : 0;
+        PT_HIP(s->shape_uv.upload(uv.data(), uv.size()));
     }
     if (first || (dirty & PT_SCENE_DIRTY_MESHES)) {
         // Device face records carry {Position0, Edge1, Edge2} (traverse.hpp
@@ -611,6 +697,7 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     D.textures = s->textures.ptr;
     D.material = s->material.ptr;
     D.shapes = s->shapes.ptr;
+    D.shape_uv = s->shape_uv.ptr;
     D.shape_nodes = reinterpret_cast<const float4*>(s->shape_nodes.ptr);
     D.mesh_faces = reinterpret_cast<const float4*>(s->faces.ptr);
     D.mesh_vertices = reinterpret_cast<const uint2*>(s->vertices.ptr);
@@ -628,16 +715,17 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     uint32_t types = s->mats & (PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_TRANSLUCENT | PT_MATS_OPENPBR);
     D.mat_classes = (types & (types - 1)) != 0 ? 1u : 0u;   // more than one material type
     // Hit records carry a mesh face's vertex indices when every index fits
-    // 21 bits (PackVertexIndices, traverse.hpp); PT_VIDX21=0 forces the
-    // face-index form (A/B testing).
-    {
-        const char* e = getenv("PT_VIDX21");
-        D.vidx21 = (p->mesh_vertex_count <= (1u << 21) && !(e && atoi(e) == 0)) ? 1u : 0u;
-    }
-    D.blas_words = BlasWordsPackable(p) ? 1u : 0u;
+    // 21 bits (PackVertexIndices, traverse.hpp); ptSetSceneHitRecordForm can
+    // force the face-index form that larger scenes use.
+    D.vidx21 = (p->mesh_vertex_count <= (1u << 21) && s->hit_record != PT_HIT_RECORD_FACE_INDEX) ? 1u : 0u;
+    // Traversal stack entries: 16-bit when every entry fits, else packed
+    // 32-bit BLAS words, else node indices (ptSetSceneStackFormat can force
+    // the wider forms, which larger scenes need).
+    D.blas_words = (s->stack_format != PT_STACK_FORMAT_NODE_INDEX && BlasWordsPackable(p)) ? 1u : 0u;
     D.blas_firstbits = 0;
     D.stack16 = 0;
-    if (uint32_t F = BlasWords16FirstBits(p)) {   // every stack entry fits 16 bits
+    uint32_t F16 = s->stack_format == PT_STACK_FORMAT_AUTO ? BlasWords16FirstBits(p) : 0u;
+    if (uint32_t F = F16) {   // every stack entry fits 16 bits
         D.blas_words = 2;
         D.blas_firstbits = F;
         D.stack16 = 1;
@@ -681,7 +769,7 @@ int ptReadSampleBuffer(pt_device* d, pt_sample_buffer* b, float* rgba)
     if (!d || !b || !rgba) { SetError("null argument"); return -1; }
     PT_HIP(hipSetDevice(d->id));
     PT_HIP(hipMemcpyAsync(rgba, b->accum, (size_t)b->width * b->height * sizeof(float4), hipMemcpyDeviceToHost, d->stream));
-    PT_HIP(hipStreamSynchronize(d->stream));
+    PT_WAIT(d);
     return 0;
 }
 
@@ -690,7 +778,7 @@ int ptWriteSampleBuffer(pt_device* d, pt_sample_buffer* b, const float* rgba)
     if (!d || !b || !rgba) { SetError("null argument"); return -1; }
     PT_HIP(hipSetDevice(d->id));
     PT_HIP(hipMemcpyAsync(b->accum, rgba, (size_t)b->width * b->height * sizeof(float4), hipMemcpyHostToDevice, d->stream));
-    PT_HIP(hipStreamSynchronize(d->stream));
+    PT_WAIT(d);
     return 0;
 }
 
@@ -719,7 +807,7 @@ int ptReadResolvedImage(pt_device* d, pt_sample_buffer* b, float* rgba)
     PT_HIP(hipSetDevice(d->id));
     PT_HIP(hipMemcpyAsync(rgba, b->display.ptr, (size_t)b->width * b->height * sizeof(float4), hipMemcpyDeviceToHost,
                           d->stream));
-    PT_HIP(hipStreamSynchronize(d->stream));
+    PT_WAIT(d);
     return 0;
 }
 
@@ -729,59 +817,14 @@ int ptReadResolvedImageSRGB8(pt_device* d, pt_sample_buffer* b, uint8_t* rgba8)
     if (!b->resolved) { SetError("sample buffer not resolved (call ptRenderSampleBuffer)"); return -1; }
     PT_HIP(hipSetDevice(d->id));
     PT_HIP(hipMemcpyAsync(rgba8, b->display8.ptr, (size_t)b->width * b->height * 4, hipMemcpyDeviceToHost, d->stream));
-    PT_HIP(hipStreamSynchronize(d->stream));
+    PT_WAIT(d);
     return 0;
 }
 
-// PT_TILE_ORDER_PERIOD (default 16): rounds between two tile-order sorts
-// (C3 / C5 / C2 at 4: +3.4 / +4.9 / -1.4 %, at 16: +3.9 / +5.3 / 0 % vs natural order).
-static uint32_t TileOrderPeriod()
-{
-    static uint32_t v = []() {
-        const char* e = getenv("PT_TILE_ORDER_PERIOD");
-        int x = e ? atoi(e) : 16;
-        return (uint32_t)(x >= 1 ? x : 16);
-    }();
-    return v;
-}
-
-// Run groups for a renderer of `tiles` 256-slot tiles: PT_RUN_GROUPS (an
-// experiment knob), else 1.  Measured on the rank-0-of-N partitions of C3
-// (tools/rehearse_scaling.py): 2-4 groups on separate streams
-// are slower at every N (N=8: 0.156 / 0.262 / 0.267 vs 0.131 ms per round),
-// since each group's extend still lasts as long as its longest tile and the
-// concurrent launches mostly serialise.
-static uint32_t RunGroups(uint32_t tiles, uint32_t cus)
-{
-    (void)cus;
-    const char* e = getenv("PT_RUN_GROUPS");
-    uint32_t g = e ? (uint32_t)std::max(1, atoi(e)) : 1u;
-    g = std::min<uint32_t>(g, pt_basic_renderer::MAX_GROUPS);
-    return std::max<uint32_t>(1u, std::min<uint32_t>(g, tiles));
-}
-
-// PT_GLOBAL_SORT=1: extend traces the frame's rays in global key order
-// (kernels.hip "Global ray sort") instead of tile by tile (TileOrder).
-static bool GlobalSortEnabled()
-{
-    const char* e = getenv("PT_GLOBAL_SORT");
-    return e && atoi(e) != 0;
-}
-
-// PT_GS_COST=0: the global sort keeps its bins in key order instead of
-// longest first by the previous round's cost (GsScan).
-static bool GlobalSortCostOrder()
-{
-    const char* e = getenv("PT_GS_COST");
-    return !(e && atoi(e) == 0);
-}
-
-// PT_TILE_ORDER=0: extend dispatches tiles in their natural order.
-static bool TileOrderEnabled()
-{
-    const char* e = getenv("PT_TILE_ORDER");
-    return !(e && atoi(e) == 0);
-}
+// Rounds between two longest-first tile-order sorts (C3 / C5 / C2 at 4:
+// +3.4 / +4.9 / -1.4 %, at 16: +3.9 / +5.3 / 0 % vs natural order; period 1
+// C3 -2.4 %: DESIGN.md §4).
+constexpr uint32_t TILE_ORDER_PERIOD = 16;
 
 pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, pt_sample_buffer* b, uint32_t rank,
                                                     uint32_t nranks)
@@ -846,53 +889,11 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     r->slots.slotof = r->slotof.ptr;
     r->slots.outcome = r->outcome.ptr;
     r->slots.tilecost = r->tilecost.ptr;
-    r->slots.order = TileOrderEnabled() && ns ? r->order.ptr : nullptr;
+    r->slots.order = ns ? r->order.ptr : nullptr;
     r->slots.done = r->done.ptr;
     r->slots.spill = nullptr;
-    r->slots.gsort = 0;
-    r->slots.perm = nullptr; r->slots.nvalid = nullptr; r->slots.key = nullptr;
-    r->slots.hist = nullptr;
-    r->slots.cls = nullptr;
-    r->slots.binprev = nullptr;
-    r->slots.gcost = 0;
     r->slots.n = ns;
-    r->slots.tile_base = 0;
     r->slots.tile_count = ns / 256;
-    r->groups = RunGroups(ns / 256, d->cu_count);
-    if (GlobalSortEnabled() && ns && r->groups == 1) {
-        const size_t nb = PT_GS_BINS + 1;
-        ok = r->perm.alloc(ns) == hipSuccess && r->nvalid.alloc(1) == hipSuccess &&
-             r->key.alloc(ns) == hipSuccess && r->hist.alloc(nb) == hipSuccess && r->cursor.alloc(nb) == hipSuccess &&
-             r->cls.alloc(ns) == hipSuccess && r->binprev.alloc(PT_GS_BINS) == hipSuccess &&
-             hipMemset(r->binprev.ptr, 0, (size_t)PT_GS_BINS * 8) == hipSuccess &&
-             hipMemset(r->tilecost.ptr, 0, ((size_t)(ns / 256) * 4 + 1) * 4) == hipSuccess &&
-             hipMemset(r->perm.ptr, 0, (size_t)ns * 4) == hipSuccess &&
-             hipMemset(r->nvalid.ptr, 0, 4) == hipSuccess &&
-             hipMemset(r->key.ptr, 0, (size_t)ns * 2) == hipSuccess && hipMemset(r->hist.ptr, 0, nb * 4) == hipSuccess &&
-             hipMemset(r->cls.ptr, 0, ns) == hipSuccess;
-        r->slots.gsort = 1;
-        r->slots.perm = r->perm.ptr; r->slots.nvalid = r->nvalid.ptr; r->slots.key = r->key.ptr;
-        r->slots.hist = r->hist.ptr; r->slots.cls = r->cls.ptr;
-        r->slots.binprev = r->binprev.ptr;
-        r->slots.gcost = GlobalSortCostOrder() ? 1u : 0u;
-        // Extend's dispatch order is then the sort's (longest-first bins);
-        // shade takes its tiles in natural order.
-        r->slots.order = nullptr;
-        if (!ok) {
-            SetError("renderer global-sort allocation failed (%u slots)", ns);
-            ptDestroyBasicRenderer(d, r);
-            return nullptr;
-        }
-    }
-    for (uint32_t g = 0; g < r->groups && r->groups > 1 && ok; g++)
-        ok = hipStreamCreateWithFlags(&r->gstream[g], hipStreamNonBlocking) == hipSuccess &&
-             hipEventCreateWithFlags(&r->gevent[g], hipEventDisableTiming) == hipSuccess;
-    if (ok && r->groups > 1) ok = hipEventCreateWithFlags(&r->fork, hipEventDisableTiming) == hipSuccess;
-    if (!ok) {
-        SetError("renderer stream creation failed");
-        ptDestroyBasicRenderer(d, r);
-        return nullptr;
-    }
     for (uint32_t band = rank; band < bands; band += nranks)
         r->pixels += (uint64_t)b->width * std::min<uint32_t>(16u, b->height - band * 16u);
     b->rank = rank;
@@ -908,19 +909,12 @@ pt_basic_renderer* ptCreateBasicRenderer(pt_device* d, pt_scene* s, pt_sample_bu
 void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
 {
     if (!r) return;
-    if (d) { (void)hipSetDevice(d->id); (void)hipStreamSynchronize(d->stream); }
+    if (d) { (void)hipSetDevice(d->id); (void)DeviceWait(d); }
     r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->lam.release();
     r->uv.release(); r->act.release(); r->pos.release(); r->slotof.release(); r->outcome.release();
     r->tilecost.release(); r->order.release();
     r->done.release();
     r->spill.release();
-    r->perm.release(); r->nvalid.release(); r->key.release(); r->hist.release(); r->cursor.release();
-    r->cls.release(); r->binprev.release();
-    for (uint32_t g = 0; g < pt_basic_renderer::MAX_GROUPS; g++) {
-        if (r->gstream[g]) (void)hipStreamDestroy(r->gstream[g]);
-        if (r->gevent[g]) (void)hipEventDestroy(r->gevent[g]);
-    }
-    if (r->fork) (void)hipEventDestroy(r->fork);
     delete r;
 }
 
@@ -962,7 +956,7 @@ static uint32_t ShadeMats(const pt_basic_renderer* r)
 static bool RoundFused(const pt_basic_renderer* r, const ptd::dslots& g)
 {
     const int mode = r->fused;
-    if (mode == 0 || g.spill || g.tile_count == 0 || g.gsort) return false;
+    if (mode == 0 || g.spill || g.tile_count == 0) return false;
     uint32_t cap = pt_round_capacity(ShadeMats(r), r->scene->d.stack16 != 0, r->dev->cu_count);
     if (cap == 0) return false;
     return mode == 2 || g.tile_count <= cap;
@@ -977,71 +971,31 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
     r->params.FrameIndex += 1;
     ptd::dparams P = Params(r, r->params.FrameIndex);
     ptd::dframe F = Frame(r);
-    const uint32_t G = r->groups, tiles = r->slots.n / 256;
-    // Group g: tiles [tiles*g/G, tiles*(g+1)/G) on its own stream, forked from
-    // and joined back into the device stream (ordering with Reset, scene
-    // updates and reads is that of one stream).
-    ptd::dslots gs[pt_basic_renderer::MAX_GROUPS];
-    hipStream_t st[pt_basic_renderer::MAX_GROUPS];
-    for (uint32_t g = 0; g < G; g++) {
-        gs[g] = r->slots;
-        gs[g].tile_base = (uint32_t)((uint64_t)tiles * g / G);
-        gs[g].tile_count = (uint32_t)((uint64_t)tiles * (g + 1) / G) - gs[g].tile_base;
-        if (gs[g].order) gs[g].order += gs[g].tile_base;
-        st[g] = G > 1 ? r->gstream[g] : d->stream;
-    }
-    if (G > 1) {
-        PT_HIP(hipEventRecord(r->fork, d->stream));
-        for (uint32_t g = 0; g < G; g++) PT_HIP(hipStreamWaitEvent(st[g], r->fork, 0));
-    }
-    // The group streams join the device stream on every exit, error paths
-    // included, so that later reads and Destroy (which synchronise the device
-    // stream only) never overlap group work.
-    auto join = [&]() -> int {
-        if (G > 1)
-            for (uint32_t g = 0; g < G; g++) {
-                PT_HIP(hipEventRecord(r->gevent[g], st[g]));
-                PT_HIP(hipStreamWaitEvent(d->stream, r->gevent[g], 0));
-            }
-        return 0;
-    };
-    auto rounds_loop = [&]() -> int {
-        for (uint32_t i = 0; i < rounds; i++) {
-            // Kernel timing samples every profile_period-th round.
-            bool sampled = d->profiling && (d->run_tick++ % d->profile_period) == 0;
-            // Tiles keep their relative cost for many rounds: re-sort every
-            // TileOrderPeriod() rounds (the sort is one small launch per group).
-            bool sort = r->slots.order && (r->order_tick++ % TileOrderPeriod()) == 0;
-            for (uint32_t g = 0; g < G; g++) {
-                event_pair ep{};
-                if (RoundFused(r, gs[g])) {
-                    if (int e = BeginTimed(d, PT_KERNEL_ROUND, ep, sampled, st[g])) return e;
-                    PT_HIP(pt_launch_round(r->scene->d, gs[g], F, P, ShadeMats(r), st[g]));
-                    if (int e = EndTimed(d, ep)) return e;
-                    if (sort) PT_HIP(pt_launch_tile_order(gs[g], st[g]));
-                    continue;
-                }
-                if (gs[g].gsort) {
-                    event_pair es{};
-                    if (int e = BeginTimed(d, PT_KERNEL_SORT, es, sampled, st[g])) return e;
-                    PT_HIP(pt_launch_gsort(gs[g], F, r->cursor.ptr, st[g]));
-                    if (int e = EndTimed(d, es)) return e;
-                }
-                if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled, st[g])) return e;
-                PT_HIP(pt_launch_extend(r->scene->d, gs[g], F, r->slots.spill, st[g]));
-                if (int e = EndTimed(d, ep)) return e;
-                if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled, st[g])) return e;
-                PT_HIP(pt_launch_shade(r->scene->d, gs[g], F, P, ShadeMats(r), st[g]));
-                if (int e = EndTimed(d, ep)) return e;
-                if (sort) PT_HIP(pt_launch_tile_order(gs[g], st[g]));
-            }
-            r->rays += r->pixels;
+    const ptd::dslots& L = r->slots;
+    const bool fused = RoundFused(r, L);
+    for (uint32_t i = 0; i < rounds; i++) {
+        // Kernel timing samples every profile_period-th round.
+        const bool sampled = d->profiling && (d->run_tick++ % d->profile_period) == 0;
+        // Tiles keep their relative cost for many rounds: re-sort every
+        // TILE_ORDER_PERIOD rounds (one small launch).
+        const bool sort = L.order && (r->order_tick++ % TILE_ORDER_PERIOD) == 0;
+        event_pair ep{};
+        if (fused) {
+            if (int e = BeginTimed(d, PT_KERNEL_ROUND, ep, sampled)) return e;
+            PT_HIP(pt_launch_round(r->scene->d, L, F, P, ShadeMats(r), d->stream));
+            if (int e = EndTimed(d, ep)) return e;
+        } else {
+            if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled)) return e;
+            PT_HIP(pt_launch_extend(r->scene->d, L, F, L.spill, d->stream));
+            if (int e = EndTimed(d, ep)) return e;
+            if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled)) return e;
+            PT_HIP(pt_launch_shade(r->scene->d, L, F, P, ShadeMats(r), d->stream));
+            if (int e = EndTimed(d, ep)) return e;
         }
-        return 0;
-    };
-    int e = rounds_loop();
-    int j = join();
-    return e ? e : j;
+        if (sort) PT_HIP(pt_launch_tile_order(L, d->stream));
+        r->rays += r->pixels;
+    }
+    return 0;
 }
 
 // k consecutive Run(1) calls: the same rounds with the same seeds (FrameIndex
@@ -1057,7 +1011,7 @@ static int RunRounds(pt_device* d, pt_basic_renderer* r, uint64_t k)
     if (!r || CheckReady(r) != 0) return -1;
     uint32_t B = r->round_batch;
     if (B == 0) B = RoundFused(r, r->slots) && r->fused == 1 ? AUTO_BATCH : 1u;
-    if (B > 1 && r->groups == 1) {
+    if (B > 1) {
         PT_HIP(hipSetDevice(d->id));
         if (int e = EnsureSpill(r)) return e;
         if (pt_rounds_available(r->slots)) {
@@ -1068,9 +1022,13 @@ static int RunRounds(pt_device* d, pt_basic_renderer* r, uint64_t k)
                 P.rounds = n;
                 P.seed_step = 1;
                 r->params.FrameIndex += n;
-                const bool sampled = d->profiling && (d->run_tick++ % d->profile_period) == 0;
+                // The profiling period counts rounds: a batch is timed when
+                // one of its n rounds is a sampled one.
+                const uint64_t t = d->run_tick % d->profile_period;
+                const bool sampled = d->profiling && (t == 0 || t + n > d->profile_period);
+                d->run_tick += n;
                 event_pair ep{};
-                if (int e = BeginTimed(d, PT_KERNEL_ROUND, ep, sampled)) return e;
+                if (int e = BeginTimed(d, PT_KERNEL_ROUNDS, ep, sampled, n)) return e;
                 PT_HIP(pt_launch_rounds(r->scene->d, r->slots, F, P, ShadeMats(r), d->stream));
                 if (int e = EndTimed(d, ep)) return e;
                 // The batch's block times order the next batch.
@@ -1100,8 +1058,6 @@ int ptSetBasicRendererRoundBatch(pt_basic_renderer* r, uint32_t rounds)
     return 0;
 }
 
-uint32_t ptBasicRendererRunGroups(pt_basic_renderer* r) { return r ? r->groups : 0; }
-
 int ptSetBasicRendererFusedRounds(pt_basic_renderer* r, int mode)
 {
     if (!r || mode < 0 || mode > 2) { SetError("ptSetBasicRendererFusedRounds: bad argument"); return -1; }
@@ -1124,7 +1080,7 @@ int ptGetStats(pt_device* d, pt_basic_renderer* r, uint64_t* rays, uint64_t* sam
 {
     if (!d || !r) { SetError("null argument"); return -1; }
     PT_HIP(hipSetDevice(d->id));
-    PT_HIP(hipStreamSynchronize(d->stream));
+    PT_WAIT(d);
     if (rays) *rays = r->rays;
     if (samples) {
         std::vector<uint32_t> w(r->slots.n / 64 + 1);
@@ -1181,7 +1137,7 @@ int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state*
 {
     if (!d || !r || !out) { SetError("null argument"); return -1; }
     PT_HIP(hipSetDevice(d->id));
-    PT_HIP(hipStreamSynchronize(d->stream));
+    PT_WAIT(d);
     uint32_t n = r->slots.n;
     std::vector<float4> ray(n), hit(n), thr(n), prob(n);
     std::vector<float> lam(n);
@@ -1219,7 +1175,6 @@ int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state*
         // Ray and hit records live at the slot's TileOrder positions (global
         // sort: both by slot).
         uint32_t qr = (s & ~255u) | (pos[s] >> 8u), qh = (s & ~255u) | (pos[s] & 255u);
-        if (r->slots.gsort) { qr = s; qh = s; }
         O.origin[0] = ray[qr].x; O.origin[1] = ray[qr].y; O.origin[2] = ray[qr].z;
         O.packed_velocity = bits(ray[qr].w);
         O.hit.time = hit[qh].x;
@@ -1312,7 +1267,7 @@ int ptRetrievePreviewQueryResult(pt_device* d, pt_preview* c, uint32_t* hit_shap
     if (!d || !c || !hit_shape_index) { SetError("null argument"); return -1; }
     PT_HIP(hipSetDevice(d->id));
     PT_HIP(hipMemcpyAsync(hit_shape_index, c->query, sizeof(uint32_t), hipMemcpyDeviceToHost, d->stream));
-    PT_HIP(hipStreamSynchronize(d->stream));
+    PT_WAIT(d);
     return 0;
 }
 
@@ -1323,7 +1278,7 @@ int ptReadPreviewImage(pt_device* d, pt_preview* c, float* rgba)
     PT_HIP(hipSetDevice(d->id));
     PT_HIP(hipMemcpyAsync(rgba, c->image.ptr, (size_t)c->width * c->height * sizeof(float4), hipMemcpyDeviceToHost,
                           d->stream));
-    PT_HIP(hipStreamSynchronize(d->stream));
+    PT_WAIT(d);
     return 0;
 }
 
@@ -1334,7 +1289,7 @@ int ptReadPreviewAOVs(pt_device* d, pt_preview* c, pt_preview_aov* aov)
     PT_HIP(hipSetDevice(d->id));
     PT_HIP(hipMemcpyAsync(aov, c->aov.ptr, (size_t)c->width * c->height * sizeof(pt_preview_aov),
                           hipMemcpyDeviceToHost, d->stream));
-    PT_HIP(hipStreamSynchronize(d->stream));
+    PT_WAIT(d);
     return 0;
 }
 
@@ -1520,11 +1475,20 @@ int ptGetKernelStats(pt_device* d, int kernel, uint64_t* launches, double* total
     return 0;
 }
 
+int ptGetKernelRounds(pt_device* d, int kernel, uint64_t* rounds)
+{
+    if (!d || !rounds || kernel < 0 || kernel >= PT_KERNEL_COUNT) { SetError("bad argument"); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    if (int e = CollectTimes(d)) return e;
+    *rounds = d->rounds[kernel];
+    return 0;
+}
+
 int ptResetKernelStats(pt_device* d)
 {
     if (!d) { SetError("null device"); return -1; }
     if (int e = CollectTimes(d)) return e;
-    for (int k = 0; k < PT_KERNEL_COUNT; k++) { d->launches[k] = 0; d->total_ms[k] = 0; }
+    for (int k = 0; k < PT_KERNEL_COUNT; k++) { d->launches[k] = 0; d->rounds[k] = 0; d->total_ms[k] = 0; }
     return 0;
 }
 
@@ -1557,39 +1521,110 @@ pt_comm* ptCommCreate(pt_device* d, int nranks, int rank, const uint8_t id[128])
     c->dev = d;
     c->nranks = nranks;
     c->rank = rank;
+    if (hipMalloc(&c->flag, sizeof(int)) != hipSuccess) { SetError("comm flag allocation failed"); delete c; return nullptr; }
     ncclResult_t e = ncclCommInitRank(&c->comm, nranks, u, rank);
-    if (e != ncclSuccess) { SetError("ncclCommInitRank: %s", ncclGetErrorString(e)); delete c; return nullptr; }
+    if (e != ncclSuccess) {
+        SetError("ncclCommInitRank: %s", ncclGetErrorString(e));
+        (void)hipFree(c->flag);
+        delete c;
+        return nullptr;
+    }
+    d->comms.push_back(c);
     return c;
 }
 
 void ptCommDestroy(pt_comm* c)
 {
     if (!c) return;
+    pt_device* d = c->dev;
+    auto& v = d->comms;
+    v.erase(std::remove(v.begin(), v.end(), c), v.end());
     if (c->comm) (void)ncclCommDestroy(c->comm);
+    if (c->flag) (void)hipFree(c->flag);
     delete c;
 }
 
+int ptCommSetTimeout(pt_comm* c, double seconds)
+{
+    if (!c || !(seconds > 0.0)) { SetError("ptCommSetTimeout: bad argument"); return -1; }
+    c->timeout_s = seconds;
+    return 0;
+}
+
+namespace {
+
+int CommUsable(pt_device* d, pt_comm* c)
+{
+    if (!d || !c) { SetError("null argument"); return -1; }
+    if (c->aborted || !c->comm) {
+        SetError("communicator aborted after an earlier failure (rank %d of %d)", c->rank, c->nranks);
+        return PT_ERROR_COMM_ABORTED;
+    }
+    if (c->dev != d) { SetError("communicator belongs to another device"); return -1; }
+    return 0;
+}
+
+// A collective was just enqueued: its synchronous result and the
+// communicator's asynchronous error state (non-blocking).  Any failure aborts
+// the device's communicators, so no rank is left inside a collective whose
+// peers have given up.
+int CommEnqueued(pt_device* d, pt_comm* c, ncclResult_t e, const char* what)
+{
+    ncclResult_t st = ncclSuccess;
+    if (e == ncclSuccess && ncclCommGetAsyncError(c->comm, &st) == ncclSuccess && (st == ncclSuccess || st == ncclInProgress))
+        return 0;
+    SetError("%s: %s; communicators aborted", what, ncclGetErrorString(e != ncclSuccess ? e : st));
+    AbortComms(d);
+    return PT_ERROR_COMM_ABORTED;
+}
+
+// Collective agreement on the caller's argument checks before a collective:
+// every rank contributes `bad` (non-zero = its check failed) to a one-word
+// max all-reduce and waits for it, so either every rank enters the
+// collective or none does (a check failing on one rank only would otherwise
+// leave the others blocked inside it).  Returns 0 when every rank passed.
+int CommAgree(pt_device* d, pt_comm* c, int bad, const char* what)
+{
+    if (c->nranks == 1) return bad ? -1 : 0;
+    int h = bad ? 1 : 0;
+    PT_HIP(hipMemcpyAsync(c->flag, &h, sizeof(int), hipMemcpyHostToDevice, d->stream));
+    ncclResult_t e = ncclAllReduce(c->flag, c->flag, 1, ncclInt32, ncclMax, c->comm, d->stream);
+    if (int r = CommEnqueued(d, c, e, what)) return r;
+    PT_HIP(hipMemcpyAsync(&h, c->flag, sizeof(int), hipMemcpyDeviceToHost, d->stream));
+    PT_WAIT(d);
+    if (h && !bad) {
+        SetError("%s: the arguments failed their check on another rank; nothing was exchanged", what);
+        return -1;
+    }
+    return h ? -1 : 0;
+}
+
+}  // namespace
+
 int ptCommReduceSampleBuffer(pt_device* d, pt_comm* c, pt_sample_buffer* b, int root)
 {
-    if (!d || !c || !b) { SetError("null argument"); return -1; }
-    if (root < 0 || root >= c->nranks) { SetError("bad root %d", root); return -1; }
-    // The rows zeroed below are those outside the buffer's partition, so the
-    // partition must be this communicator's rank of nranks.  A whole-frame
-    // buffer on a multi-rank communicator is a sample shard: reducing it in
-    // place would add the root's previous totals again on a repeated call.
-    if (b->nranks == 1 && c->nranks > 1) {
+    if (int e = CommUsable(d, c)) return e;
+    PT_HIP(hipSetDevice(d->id));
+    // Argument checks, agreed on by every rank (CommAgree).  The rows zeroed
+    // below are those outside the buffer's partition, so the partition must
+    // be this communicator's rank of nranks.  A whole-frame buffer on a
+    // multi-rank communicator is a sample shard: reducing it in place would
+    // add the root's previous totals again on a repeated call.  (A one-rank
+    // communicator sums nothing across ranks; it may reduce any partition --
+    // the zeroing alone is then observable.)
+    int bad = 0;
+    if (!b) { SetError("null sample buffer"); bad = 1; }
+    else if (root < 0 || root >= c->nranks) { SetError("bad root %d", root); bad = 1; }
+    else if (b->nranks == 1 && c->nranks > 1) {
         SetError("ptCommReduceSampleBuffer: whole-frame buffer on a %d-rank communicator (sample shards: use "
                  "ptCommReduceSampleBufferInto)", c->nranks);
-        return -1;
-    }
-    // (A one-rank communicator sums nothing across ranks; it may reduce any
-    // partition -- the zeroing alone is then observable.)
-    if (c->nranks > 1 && b->nranks > 1 && ((int)b->nranks != c->nranks || (int)b->rank != c->rank)) {
+        bad = 1;
+    } else if (c->nranks > 1 && b->nranks > 1 && ((int)b->nranks != c->nranks || (int)b->rank != c->rank)) {
         SetError("sample buffer partition %u/%u does not match communicator rank %d of %d", b->rank, b->nranks,
                  c->rank, c->nranks);
-        return -1;
+        bad = 1;
     }
-    PT_HIP(hipSetDevice(d->id));
+    if (int e = CommAgree(d, c, bad, "ptCommReduceSampleBuffer")) return e;
     size_t count = (size_t)b->width * b->height * 4;
     // Only the bands this rank renders may enter the sum: at the root the
     // other rows hold the previous reduce's totals (a progressive frame
@@ -1597,25 +1632,26 @@ int ptCommReduceSampleBuffer(pt_device* d, pt_comm* c, pt_sample_buffer* b, int 
     // in-place sum stays exact on every call.
     PT_HIP(pt_launch_zero_unowned(b->accum, b->width, b->height, b->rank, b->nranks, d->stream));
     ncclResult_t e = ncclReduce(b->accum, b->accum, count, ncclFloat32, ncclSum, root, c->comm, d->stream);
-    if (e != ncclSuccess) { SetError("ncclReduce: %s", ncclGetErrorString(e)); return (int)e; }
-    return 0;
+    return CommEnqueued(d, c, e, "ncclReduce");
 }
 
 int ptCommReduceSampleBufferInto(pt_device* d, pt_comm* c, pt_sample_buffer* b, pt_sample_buffer* total, int root)
 {
-    if (!d || !c || !b) { SetError("null argument"); return -1; }
-    if (root < 0 || root >= c->nranks) { SetError("bad root %d", root); return -1; }
-    const bool is_root = c->rank == root;
-    if (is_root && (!total || total->width != b->width || total->height != b->height)) {
-        SetError("ptCommReduceSampleBufferInto: the root needs a total buffer of the same size");
-        return -1;
-    }
+    if (int e = CommUsable(d, c)) return e;
     PT_HIP(hipSetDevice(d->id));
+    const bool is_root = c->rank == root;
+    int bad = 0;
+    if (!b) { SetError("null sample buffer"); bad = 1; }
+    else if (root < 0 || root >= c->nranks) { SetError("bad root %d", root); bad = 1; }
+    else if (is_root && (!total || total->width != b->width || total->height != b->height)) {
+        SetError("ptCommReduceSampleBufferInto: the root needs a total buffer of the same size");
+        bad = 1;
+    }
+    if (int e = CommAgree(d, c, bad, "ptCommReduceSampleBufferInto")) return e;
     size_t count = (size_t)b->width * b->height * 4;
     ncclResult_t e = ncclReduce(b->accum, is_root ? total->accum : b->accum, count, ncclFloat32, ncclSum, root, c->comm,
                                 d->stream);
-    if (e != ncclSuccess) { SetError("ncclReduce: %s", ncclGetErrorString(e)); return (int)e; }
-    return 0;
+    return CommEnqueued(d, c, e, "ncclReduce");
 }
 
 // The same frame-end exchange with 1/N of the traffic: the bands are
@@ -1627,14 +1663,17 @@ int ptCommReduceSampleBufferInto(pt_device* d, pt_comm* c, pt_sample_buffer* b, 
 // instead of a ring reduction of the whole buffer.
 int ptCommGatherSampleBuffer(pt_device* d, pt_comm* c, pt_sample_buffer* b, int root)
 {
-    if (!d || !c || !b) { SetError("null argument"); return -1; }
-    if (root < 0 || root >= c->nranks) { SetError("bad root %d", root); return -1; }
-    if ((int)b->nranks != c->nranks || (int)b->rank != c->rank) {
+    if (int e = CommUsable(d, c)) return e;
+    PT_HIP(hipSetDevice(d->id));
+    int bad = 0;
+    if (!b) { SetError("null sample buffer"); bad = 1; }
+    else if (root < 0 || root >= c->nranks) { SetError("bad root %d", root); bad = 1; }
+    else if ((int)b->nranks != c->nranks || (int)b->rank != c->rank) {
         SetError("sample buffer partition %u/%u does not match communicator rank %d of %d", b->rank, b->nranks,
                  c->rank, c->nranks);
-        return -1;
+        bad = 1;
     }
-    PT_HIP(hipSetDevice(d->id));
+    if (int e = CommAgree(d, c, bad, "ptCommGatherSampleBuffer")) return e;
     if (c->nranks == 1) return 0;
     uint32_t bands = (b->height + 15) / 16;
     ncclResult_t e = ncclGroupStart();
@@ -1649,8 +1688,7 @@ int ptCommGatherSampleBuffer(pt_device* d, pt_comm* c, pt_sample_buffer* b, int 
     }
     ncclResult_t g = ncclGroupEnd();
     if (e == ncclSuccess) e = g;
-    if (e != ncclSuccess) { SetError("band gather: %s", ncclGetErrorString(e)); return (int)e; }
-    return 0;
+    return CommEnqueued(d, c, e, "band gather");
 }
 
 }  // extern "C"

@@ -595,8 +595,11 @@ PT_DEV float4 CompactHit(const lane_state& Ln, bool vidx21)
 
 // Hit attribute reconstruction (scene.glsl.inc:535-608).  Mesh faces: the
 // vertex indices come packed in the hit record (vidx21) or from the face.
+// uv = false: the caller never reads the texture coordinates (the hit
+// shape's material samples no texture, dscene::shape_uv), which are then left
+// 0 instead of computed (a sphere's atan2, a mesh's three vertex V loads).
 PT_DEV void HitAttributesV(const dscene& S, uint32_t ShapeIndex, bool packed, uint32_t Z, uint32_t Wd, pt3 C,
-                           uint32_t& Material, pt3& Normal, pt3& TangentX, pt2& UV);
+                           uint32_t& Material, pt3& Normal, pt3& TangentX, pt2& UV, bool uv = true);
 
 PT_DEV void HitAttributes(const dscene& S, uint32_t ShapeIndex, uint32_t Prim, pt3 C, uint32_t& Material, pt3& Normal,
                           pt3& TangentX, pt2& UV)
@@ -606,20 +609,23 @@ PT_DEV void HitAttributes(const dscene& S, uint32_t ShapeIndex, uint32_t Prim, p
 
 // From a compact hit record (h = {Time, Shape, z, w}, c = {C.y, C.z}).
 PT_DEV void HitAttributesRecord(const dscene& S, uint32_t ShapeIndex, float4 h, float2 c, uint32_t& Material,
-                                pt3& Normal, pt3& TangentX, pt2& UV)
+                                pt3& Normal, pt3& TangentX, pt2& UV, bool uv = true)
 {
     const bool mesh = S.shapes[ShapeIndex].Type == PT_SHAPE_TYPE_MESH_INSTANCE;
     if (S.vidx21) {
         pt3 C = mesh ? v3(1 - c.x - c.y, c.x, c.y) : v3(h.z, c.x, c.y);
-        HitAttributesV(S, ShapeIndex, true, __float_as_uint(h.z), __float_as_uint(h.w), C, Material, Normal, TangentX, UV);
+        HitAttributesV(S, ShapeIndex, true, __float_as_uint(h.z), __float_as_uint(h.w), C, Material, Normal, TangentX, UV,
+                       uv);
     } else {
-        HitAttributesV(S, ShapeIndex, false, __float_as_uint(h.z), 0u, v3(h.w, c.x, c.y), Material, Normal, TangentX, UV);
+        HitAttributesV(S, ShapeIndex, false, __float_as_uint(h.z), 0u, v3(h.w, c.x, c.y), Material, Normal, TangentX, UV,
+                       uv);
     }
 }
 
 PT_DEV void HitAttributesV(const dscene& S, uint32_t ShapeIndex, bool packed, uint32_t Z, uint32_t Wd, pt3 C,
-                           uint32_t& Material, pt3& Normal, pt3& TangentX, pt2& UV)
+                           uint32_t& Material, pt3& Normal, pt3& TangentX, pt2& UV, bool uv)
 {
+    UV = v2(0.0f, 0.0f);
     const pt_packed_shape* Shape = &S.shapes[ShapeIndex];
     Material = Shape->MaterialIndex;
     int32_t Type = Shape->Type;
@@ -642,21 +648,25 @@ PT_DEV void HitAttributesV(const dscene& S, uint32_t ShapeIndex, bool packed, ui
         pt3 N = SafeNormalize(xyz(A0) * C.x + xyz(A1) * C.y + xyz(A2) * C.z);
         Normal = TransformNormal(N, From);
         TangentX = ComputeTangentVector(Normal);
-        pt2 UV0 = v2(A0.w, S.vertex_v[i0]);
-        pt2 UV1 = v2(A1.w, S.vertex_v[i1]);
-        pt2 UV2 = v2(A2.w, S.vertex_v[i2]);
-        UV = UV0 * C.x + UV1 * C.y + UV2 * C.z;
+        if (uv) {
+            pt2 UV0 = v2(A0.w, S.vertex_v[i0]);
+            pt2 UV1 = v2(A1.w, S.vertex_v[i1]);
+            pt2 UV2 = v2(A2.w, S.vertex_v[i2]);
+            UV = UV0 * C.x + UV1 * C.y + UV2 * C.z;
+        }
     } else if (Type == PT_SHAPE_TYPE_PLANE) {
         Normal = TransformNormal(v3(0, 0, 1), From);
         TangentX = TransformDirection(v3(1, 0, 0), To);
-        UV = v2(pt_fract(C.x), pt_fract(C.y));
+        if (uv) UV = v2(pt_fract(C.x), pt_fract(C.y));
     } else if (Type == PT_SHAPE_TYPE_SPHERE) {
         pt3 P = C;
-        float U = (pt_atan2(P.y, P.x) + PT_PI) / PT_TAU;
-        float W = (P.z + 1.0f) / 2.0f;
         Normal = TransformNormal(P, From);
         TangentX = TransformDirection(cross(P, v3(-P.y, P.x, 0)), To);
-        UV = v2(U, W);
+        if (uv) {
+            float U = (pt_atan2(P.y, P.x) + PT_PI) / PT_TAU;
+            float W = (P.z + 1.0f) / 2.0f;
+            UV = v2(U, W);
+        }
     } else {
         pt3 P = C;
         pt3 Q = vabs(P);

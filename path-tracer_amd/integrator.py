@@ -63,6 +63,13 @@ class Device:
         _check(N.hip_lib().ptGetKernelStats(self._h, kernel, C.byref(n), C.byref(ms)), "ptGetKernelStats")
         return int(n.value), float(ms.value)
 
+    def kernel_rounds(self, kernel: int) -> int:
+        """Rounds covered by the timed launches of `kernel` (a round batch
+        covers several): total_ms / rounds is its time per round."""
+        n = C.c_uint64(0)
+        _check(N.hip_lib().ptGetKernelRounds(self._h, kernel, C.byref(n)), "ptGetKernelRounds")
+        return int(n.value)
+
     def reset_kernel_stats(self):
         _check(N.hip_lib().ptResetKernelStats(self._h), "ptResetKernelStats")
 
@@ -95,6 +102,14 @@ class DeviceScene:
     @property
     def handle(self):
         return self._h
+
+    def set_stack_format(self, fmt: int):
+        """PT_STACK_FORMAT_* (0 auto, 1 packed 32-bit words, 2 node indices); next update()."""
+        _check(N.hip_lib().ptSetSceneStackFormat(self._h, int(fmt)), "ptSetSceneStackFormat")
+
+    def set_hit_record_form(self, form: int):
+        """PT_HIT_RECORD_* (0 auto, 1 face index); next update()."""
+        _check(N.hip_lib().ptSetSceneHitRecordForm(self._h, int(form)), "ptSetSceneHitRecordForm")
 
     def update(self, scene, dirty_flags: int = 0xFFFFFFFF):
         packs = scene.packs() if hasattr(scene, "packs") else scene
@@ -234,11 +249,6 @@ class BasicRenderer:
     @property
     def slot_count(self) -> int:
         return int(N.hip_lib().ptBasicRendererSlotCount(self._h))
-
-    @property
-    def run_groups(self) -> int:
-        """Tile groups advanced on separate streams (ptBasicRendererRunGroups)."""
-        return int(N.hip_lib().ptBasicRendererRunGroups(self._h))
 
     def set_fused_rounds(self, mode: int):
         """0 never / 1 automatic / 2 whenever possible (ptSetBasicRendererFusedRounds)."""
@@ -389,6 +399,12 @@ class Comm:
         self._h = L.ptCommCreate(device.handle, nranks, rank, buf)
         if not self._h:
             raise PathTracerError(L.ptGetLastError().decode())
+
+    def set_timeout(self, seconds: float):
+        """Deadline of a device-stream wait while this communicator is live
+        (ptCommSetTimeout; default 600 s).  Past it the communicators are
+        aborted and the waiting call raises (PT_ERROR_TIMEOUT)."""
+        _check(N.hip_lib().ptCommSetTimeout(self._h, float(seconds)), "ptCommSetTimeout")
 
     @staticmethod
     def unique_id() -> bytes:

@@ -34,3 +34,18 @@ def test_gpus2_self_launches_two_ranks():
 def test_world_size_must_match_gpus():
     p = run_bench(["--gpus", "4", "--launch-check"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode == 2 and "WORLD_SIZE=2 but --gpus 4" in p.stderr
+
+
+def test_failing_rank_ends_launch_nonzero():
+    """Failure path: a rank that raises before the
+    frame-end exchange, while its peer is blocked in it, ends the whole
+    N-rank launch with a non-zero status within a bound (the launcher stops
+    the surviving rank; nothing waits for a collective that cannot finish)."""
+    import time
+    t0 = time.perf_counter()
+    p = run_bench(["--gpus", "2", "--launch-check", "--inject-failure", "1"])
+    dt = time.perf_counter() - t0
+    assert p.returncode != 0
+    assert "injected failure on rank 1" in p.stderr
+    assert not [l for l in p.stdout.splitlines() if l.startswith("{")]   # no result line
+    assert dt < 90.0, f"failed launch took {dt:.1f} s to end"

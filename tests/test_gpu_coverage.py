@@ -375,6 +375,43 @@ def test_comm_gather_single_rank_and_partition_check(pt, dev):
     s.close()
 
 
+def test_comm_error_contract_single_rank(pt, dev):
+    """The exchange's failure contract on a one-rank communicator (INTEGRATION
+    §3): a failed argument check (bad root, mismatched partition, missing total
+    buffer) fails the call before any collective and leaves the communicator
+    usable; ptCommSetTimeout rejects a non-positive deadline; with the
+    communicator live, waits go through the polling path and still complete."""
+    s = pt.Scene.config(1)
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    sb = pt.SampleBuffer(dev, 48, 40)
+    total = pt.SampleBuffer(dev, 48, 40)
+    r = pt.BasicRenderer(dev, ds, sb)
+    r.RenderFlags = 3
+    comm = pt.Comm(dev, 1, 0, pt.Comm.unique_id())
+    comm.set_timeout(120.0)
+    with pytest.raises(pt.PathTracerError):
+        comm.set_timeout(0.0)
+    r.reset()
+    r.run(2)
+    dev.synchronize()                                       # polling wait (live communicator)
+    with pytest.raises(pt.PathTracerError, match="bad root"):
+        comm.reduce_sample_buffer_into(sb, total, 1)
+    with pytest.raises(pt.PathTracerError, match="total buffer"):
+        comm.reduce_sample_buffer_into(sb, None, 0)
+    with pytest.raises(pt.PathTracerError, match="bad root"):
+        comm.gather_sample_buffer(sb, 3)
+    comm.reduce_sample_buffer_into(sb, total, 0)            # still usable
+    dev.synchronize()
+    assert np.array_equal(bits(total.read()), bits(sb.read()))
+    rounds, samples = r.render_frame(4 * 48 * 40, 1000)     # ptRenderFrame's waits poll too
+    assert samples >= 4 * 48 * 40
+    comm.close()
+    for x in (r, total, sb, ds):
+        x.close()
+    s.close()
+
+
 def test_sample_shard_offset_and_reduce_into(pt, dev):
     """Sample sharding (bench.py's default multi-GPU split): a renderer whose
     RNG stream starts at FrameIndex 1 << 24 (rank 1's) is bit-exact against the
@@ -452,16 +489,15 @@ def test_two_process_sample_shards_equal_summed_renders(pt, dev, tmp_path):
     s.close()
 
 
-@pytest.mark.parametrize("vidx21", ["0", "1"])
-def test_hit_record_forms_bit_exact(pt, dev, monkeypatch, vidx21):
+@pytest.mark.parametrize("form", [1, 0], ids=["face-index", "vertex-indices"])
+def test_hit_record_forms_bit_exact(pt, dev, form):
     """Both compact hit-record forms (packed vertex indices, the default for
     scenes whose vertex indices fit 21 bits, and the face-index form that
-    larger scenes use; PT_VIDX21=0 forces it) give the oracle's state and
-    image, meshes and analytic shapes alike (C5 mixes both)."""
-    monkeypatch.setenv("PT_VIDX21", vidx21)
+    larger scenes use; ptSetSceneHitRecordForm forces it) give the oracle's
+    state and image, meshes and analytic shapes alike (C5 mixes both)."""
     for cfg, W, H in ((3, 160, 96), (5, 128, 64)):
         s = pt.Scene.config(cfg)
-        gs, os_, ga, oa = render_pair(pt, dev, cfg, W, H, [2, 1, 1], scene=s)
+        gs, os_, ga, oa = render_pair(pt, dev, cfg, W, H, [2, 1, 1], scene=s, hit_record=form)
         compare_state(gs, os_)
         assert np.array_equal(bits(ga), bits(oa))
         s.close()

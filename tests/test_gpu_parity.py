@@ -62,21 +62,20 @@ def test_trace_rays_bit_exact(pt, dev, config):
     ds.close()
 
 
-@pytest.mark.parametrize("env", [{}, {"PT_STACK16": "0"}, {"PT_STACK16": "0", "PT_BLAS_WORDS": "0"}],
-                         ids=["stack16", "stack32-packed", "stack32-node-index"])
-def test_stack_formats_bit_exact(pt, dev, monkeypatch, env):
+@pytest.mark.parametrize("fmt", [0, 1, 2], ids=["stack16", "stack32-packed", "stack32-node-index"])
+def test_stack_formats_bit_exact(pt, dev, fmt):
     """Every traversal-stack entry format (chosen per scene at upload: 16-bit
-    packed words, 32-bit packed words, node indices) gives the same hits."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+    packed words, 32-bit packed words, node indices; ptSetSceneStackFormat
+    forces the wider ones) gives the same hits."""
     for config in (3, 5):
         s = scene_for(pt, config)
         ds = pt.DeviceScene(dev)
+        ds.set_stack_format(fmt)
         ds.update(s)
         o, v, d = random_rays(s.arrays(), 20000, seed=10 + config)
         compare_hits(ds.trace_rays(o, v, d), oracle_lib.trace_rays(s.packs(), o, v, d))
         ds.close()
-    gs, os_, ga, oa = render_pair(pt, dev, 5, 128, 64, [2, 1])
+    gs, os_, ga, oa = render_pair(pt, dev, 5, 128, 64, [2, 1], stack_format=fmt)
     compare_state(gs, os_)
     assert np.array_equal(ga.view(np.uint32), oa.view(np.uint32))
 
@@ -113,12 +112,16 @@ def test_deep_stack_spills_bit_exact(pt, dev, tmp_path):
 
 
 def render_pair(pt, dev, config, W, H, schedule, camera=0, flags=3, termination=0.0, rank=0, nranks=1,
-                scene=None, fused=None):
+                scene=None, fused=None, stack_format=0, hit_record=0):
     """The same Reset + Run(schedule...) on the HIP renderer and the oracle:
     (GPU state, oracle state, GPU accumulator, oracle accumulator).
-    fused: the renderer's fused-rounds mode (None: its default)."""
+    fused: the renderer's fused-rounds mode (None: its default);
+    stack_format / hit_record: the device scene's encodings (PT_STACK_FORMAT_*,
+    PT_HIT_RECORD_*; 0 = automatic)."""
     s = scene if scene is not None else scene_for(pt, config)
     ds = pt.DeviceScene(dev)
+    ds.set_stack_format(stack_format)
+    ds.set_hit_record_form(hit_record)
     ds.update(s)
     sb = pt.SampleBuffer(dev, W, H)
     r = pt.BasicRenderer(dev, ds, sb, rank=rank, nranks=nranks)
@@ -242,8 +245,9 @@ def test_profiling_counts_kernels(pt, dev):
     r.run(3)
     n_ext, ms_ext = dev.kernel_stats(1)
     n_sh, ms_sh = dev.kernel_stats(2)
-    # one extend + one shade per round and tile range (run groups)
-    assert n_ext == n_sh and n_ext % 3 == 0 and n_ext >= 3 and ms_ext > 0 and ms_sh > 0
+    # one extend + one shade per round
+    assert n_ext == n_sh == 3 and ms_ext > 0 and ms_sh > 0
+    assert dev.kernel_rounds(1) == 3 and dev.kernel_rounds(2) == 3
     # a 64x64 frame fits the GPU at once: the automatic mode fuses its rounds
     # into one launch each (kernel 5)
     dev.reset_kernel_stats()
@@ -251,7 +255,20 @@ def test_profiling_counts_kernels(pt, dev):
     r.run(2)
     n_rd, ms_rd = dev.kernel_stats(5)
     assert dev.kernel_stats(1)[0] == 0 and dev.kernel_stats(2)[0] == 0
-    assert n_rd >= 2 and n_rd % 2 == 0 and ms_rd > 0
+    assert n_rd == 2 and dev.kernel_rounds(5) == 2 and ms_rd > 0
+    # consecutive Run(1) rounds of such a frame run as 16-round batches
+    # (kernel 6, PT_KERNEL_ROUNDS): a timed batch counts its rounds, and the
+    # profiling period counts rounds (period 8: every batch holds a sampled
+    # round), so time per round = total / rounds.
+    dev.set_profiling(True, period=8)
+    dev.reset_kernel_stats()
+    r.run_rounds(40)
+    n_b, ms_b = dev.kernel_stats(6)
+    assert n_b == 3 and dev.kernel_rounds(6) == 40 and ms_b > 0
+    dev.set_profiling(True, period=32)
+    dev.reset_kernel_stats()
+    r.run_rounds(64)    # batches of rounds 0-15, 16-31, 32-47, 48-63: rounds 0 and 32 sampled
+    assert dev.kernel_stats(6)[0] == 2 and dev.kernel_rounds(6) == 32
     dev.set_profiling(False)
     r.close(); sb.close(); ds.close()
 
