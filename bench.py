@@ -58,6 +58,7 @@ KERNEL_IDS = {"extend": 1, "shade": 2, "round": 5, "rounds": 6}   # pt_api.h PT_
 L2_PEAK_GBPS = 34500.0   # aggregate L2 bandwidth (MI355X_MICROARCH.md § L2)
 PATH_BYTES_PER_RAY = 220  # SURVEY.md §8(d) whole-path definition
 STEADY_ROUNDS = 64        # secondary key: steady-state rounds timed after the frames
+FILL_SLOTS = 1 << 21      # slots per launch a band partition is filled to with path streams (C3 frame: 2.07 M)
 SETTLE_ROUNDS = 32        # ... after this many rounds past a restart
 
 
@@ -195,6 +196,8 @@ def main():
                     help="every rank on device 0 (multi-rank flow check on a one-GPU box; timings not meaningful)")
     ap.add_argument("--launch-check", action="store_true",
                     help="N-rank launch plumbing only (gloo, no GPU): CPU test of the launcher")
+    ap.add_argument("--streams", type=int, default=0,
+                    help="path streams per owned pixel (0: auto -- bands fill ~2^21 slots per launch, samples 1)")
     ap.add_argument("--inject-failure", type=int, default=-1, metavar="RANK",
                     help="with --launch-check: this rank raises before the exchange (tests the failure path)")
     ap.add_argument("--shard", choices=("auto", "samples", "bands"), default="auto",
@@ -239,17 +242,23 @@ def main():
     dscene.update(scene)
     sb = pt.SampleBuffer(dev, width, height)
     part_rank, part_n = (rank, world) if shard == "bands" else (0, 1)
-    r = pt.BasicRenderer(dev, dscene, sb, rank=part_rank, nranks=part_n)
+    px_owned = int(np.sum(pt.owned_pixels(width, height, part_rank, part_n)))
+    # Path streams per owned pixel (bands): a partition smaller than one GPU's
+    # fill carries several independent paths per pixel so that each launch
+    # still holds about FILL_SLOTS slots.
+    streams = args.streams if args.streams > 0 else (
+        max(1, round(FILL_SLOTS / max(px_owned, 1))) if shard == "bands" else 1)
+    r = pt.BasicRenderer(dev, dscene, sb, rank=part_rank, nranks=part_n, streams=streams)
     r.RenderFlags = info.render_flags
     r.PathTerminationProbability = info.termination_probability
     # Sample shards: rank r's RNG stream starts at FrameIndex r << 24 (seeds
     # are hashed from (x, y, FrameIndex), scene.glsl.inc / basic.cpp:285-332).
     if shard == "samples":
         r.FrameIndex = rank << 24
-    slots_owned = int(np.sum(pt.owned_pixels(width, height, part_rank, part_n)))
+    slots_owned = px_owned * streams    # paths (rays) per round
     # This rank's frame target (Σ alpha): samples -> 1/N of spp x frame,
     # bands -> spp x its own pixels.
-    target = math.ceil(spp * width * height / world) if shard == "samples" else spp * slots_owned
+    target = math.ceil(spp * width * height / world) if shard == "samples" else spp * px_owned
     total = pt.SampleBuffer(dev, width, height) if (world > 1 and shard == "samples" and rank == 0) else None
     comm = None
     exchange = None
@@ -314,6 +323,7 @@ def main():
             last_note[0] = now
         if samples < target:
             raise RuntimeError(f"frame stopped at {rounds} rounds with {samples} of {target} samples")
+        r.merge_streams()    # path streams -> the sample buffer (no-op for one stream)
         frame_end_exchange()
         if record:
             frames.append((rounds, samples))
@@ -429,7 +439,8 @@ def main():
         "config": {
             "workload": (f"C{args.config} scene, one {width}x{height} {spp}-spp frame per step (Reset, Run(2), "
                          f"Run(1) until the frame's sample count reaches {spp} x pixels), split in 16-row bands over "
-                         f"{world} GPU(s) ({slots_owned} px on rank 0) + the bands' gather to rank 0"
+                         f"{world} GPU(s) ({px_owned} px on rank 0, {streams} path stream(s) per pixel) + the bands' "
+                         f"gather to rank 0"
                          if shard == "bands" else
                          f"C{args.config} scene, one {width}x{height} {spp}-spp frame per step (Reset, Run(2), "
                          f"Run(1) until the frame's sample count reaches {spp} x pixels); each of {world} GPU(s) "
@@ -439,6 +450,8 @@ def main():
             "exchange": exchange,
             "comm_ranks": comm_ranks,
             "spp_target": spp,
+            "streams": streams,
+            "slots_per_launch_rank0": slots_owned,
             "frame_target_samples_rank0": target,
             "mesh_faces": info.mesh_face_count,
             "parallelism": (f"pixel-bands x{world}" + (f" + {xname} band gather to rank 0" if world > 1 else "")

@@ -201,6 +201,20 @@ pt_basic_renderer* ptCreateBasicRenderer(pt_device* device, pt_scene* scene, pt_
 /* Renderer owning only the 16-row pixel bands b with b % nranks == rank. */
 pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* device, pt_scene* scene, pt_sample_buffer* buffer,
                                                     uint32_t rank, uint32_t nranks);
+/* Path streams for a partition too small to fill the GPU:
+ * the renderer carries `streams` independent paths per owned pixel, stream k
+ * seeded with FrameIndex + (k << 24) -- the sample shards' offsets -- so one
+ * launch holds streams x the partition's slots.  With more than one stream
+ * each stream accumulates into an accumulator of its own, and
+ * ptMergeBasicRendererStreams writes their sum, in stream order, into the
+ * sample buffer's owned pixels (call it before reading or exchanging a
+ * frame; it may repeat as the rounds go on).  Each stream's state and
+ * accumulator equal a one-stream renderer's started at its FrameIndex
+ * offset. */
+pt_basic_renderer* ptCreateBasicRendererStreams(pt_device* device, pt_scene* scene, pt_sample_buffer* buffer,
+                                                uint32_t rank, uint32_t nranks, uint32_t streams);
+int                ptMergeBasicRendererStreams(pt_device* device, pt_basic_renderer* renderer);
+uint32_t           ptBasicRendererStreams(pt_basic_renderer* renderer);
 void               ptDestroyBasicRenderer(pt_device* device, pt_basic_renderer* renderer);
 pt_basic_renderer_params* ptBasicRendererParams(pt_basic_renderer* renderer);
 int                ptResetBasicRenderer(pt_device* device, pt_basic_renderer* renderer);
@@ -243,8 +257,11 @@ int                ptGetStats(pt_device* device, pt_basic_renderer* renderer, ui
 int                ptRenderFrame(pt_device* device, pt_basic_renderer* renderer, uint64_t target_samples,
                                  uint32_t max_rounds, uint32_t* rounds_out, uint64_t* samples_out);
 /* out = width*height states in image order; pixels outside the renderer's
- * partition are left untouched. */
+ * partition are left untouched.  Stream 0's paths (ptReadBasicRendererStreamState:
+ * any stream's). */
 int                ptReadBasicRendererState(pt_device* device, pt_basic_renderer* renderer, pt_pixel_state* out);
+int                ptReadBasicRendererStreamState(pt_device* device, pt_basic_renderer* renderer, uint32_t stream,
+                                                  pt_pixel_state* out);
 
 /* Editor preview (preview_render.glsl:96-178): one primary ray per pixel of
  * RenderSizeX x RenderSizeY through the same Trace() as the integrator.

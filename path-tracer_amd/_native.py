@@ -230,6 +230,10 @@ HIP_API = {
     "ptReadResolvedImageSRGB8": (_i32, [_vp, _vp, C.POINTER(C.c_uint8)]),
     "ptCreateBasicRenderer": (_vp, [_vp, _vp, _vp]),
     "ptCreateBasicRendererPartitioned": (_vp, [_vp, _vp, _vp, _u32, _u32]),
+    "ptCreateBasicRendererStreams": (_vp, [_vp, _vp, _vp, _u32, _u32, _u32]),
+    "ptMergeBasicRendererStreams": (_i32, [_vp, _vp]),
+    "ptBasicRendererStreams": (_u32, [_vp]),
+    "ptReadBasicRendererStreamState": (_i32, [_vp, _vp, _u32, _vp]),
     "ptDestroyBasicRenderer": (None, [_vp, _vp]),
     "ptBasicRendererParams": (C.POINTER(pt_basic_renderer_params), [_vp]),
     "ptResetBasicRenderer": (_i32, [_vp, _vp]),

@@ -89,9 +89,27 @@ PT_DEV uint32_t TileRow(const dframe& F, uint32_t t)
     return F.tiles_x == 1 ? t : __umulhi(t, F.tiles_x_magic);
 }
 
-PT_DEV bool SlotPixel(const dframe& F, uint32_t s, uint32_t& x, uint32_t& y)
+// Path stream of tile t, and t's tile within its stream.
+PT_DEV uint32_t TileStream(const dframe& F, uint32_t& t)
+{
+    if (F.streams == 1) return 0;
+    const uint32_t k = __umulhi(t, F.stream_magic);
+    t -= k * F.stream_tiles;
+    return k;
+}
+
+// The seed of slot s's stream (FrameIndex + (stream << 24)) and its
+// accumulator.
+PT_DEV uint32_t StreamSeed(uint32_t seed, uint32_t stream) { return seed + (stream << 24); }
+PT_DEV float4* StreamAccum(const dframe& F, uint32_t stream)
+{
+    return F.streams == 1 ? F.accum : F.accx + (size_t)stream * F.width * F.height;
+}
+
+PT_DEV bool SlotPixel(const dframe& F, uint32_t s, uint32_t& x, uint32_t& y, uint32_t& stream)
 {
     uint32_t t = s >> 8, l = s & 255u;
+    stream = TileStream(F, t);
     uint32_t k = TileRow(F, t);
     uint32_t tx = t - k * F.tiles_x;
     uint32_t band = F.rank + k * F.nranks;
@@ -102,9 +120,16 @@ PT_DEV bool SlotPixel(const dframe& F, uint32_t s, uint32_t& x, uint32_t& y)
 
 // Valid positions of a tile are the first (pixels of the tile inside the
 // image): TileOrder sorts the slots outside the image to the end.
+PT_DEV bool SlotPixel(const dframe& F, uint32_t s, uint32_t& x, uint32_t& y)
+{
+    uint32_t stream;
+    return SlotPixel(F, s, x, y, stream);
+}
+
 PT_DEV bool PositionValid(const dframe& F, uint32_t q)
 {
     uint32_t t = q >> 8;
+    (void)TileStream(F, t);
     uint32_t k = TileRow(F, t);
     uint32_t tx = t - k * F.tiles_x;
     uint32_t band = F.rank + k * F.nranks;
@@ -932,14 +957,14 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
 __global__ __launch_bounds__(256) void raygen_kernel(dscene S, dslots L, dframe F, dparams Pm)
 {
     uint32_t s = blockIdx.x * 256 + threadIdx.x;
-    uint32_t x, y;
-    bool valid = SlotPixel(F, s, x, y);
+    uint32_t x, y, stream;
+    bool valid = SlotPixel(F, s, x, y, stream);
     pt3 O = v3s(0), V = v3s(0);
     if (valid) {
         rng G;
-        G.State = pt_seed(x, y, Pm.seed);
+        G.State = pt_seed(x, y, StreamSeed(Pm.seed, stream));
         GenerateNewPath(S, L, F, Pm, G, s, x, y, O, V);
-        F.accum[(size_t)y * F.width + x] = make_float4(0, 0, 0, 0);
+        StreamAccum(F, stream)[(size_t)y * F.width + x] = make_float4(0, 0, 0, 0);
     }
     TileOrderStoreRay(L, s, valid, O, V, L.pos[s] & 255u);
 }
@@ -1176,6 +1201,27 @@ __global__ __launch_bounds__(256) void atlas_tile_kernel(const float4* src, floa
     }
 }
 
+// Path streams' merge (ptMergeBasicRendererStreams): for every pixel of the
+// renderer's bands, accum = ((accx[0] + accx[1]) + accx[2]) ... in stream
+// order; the streams' own accumulators keep running.
+__global__ __launch_bounds__(256) void merge_streams_kernel(float4* accum, float4* accx, uint32_t width, uint32_t height,
+                                                            uint32_t rank, uint32_t nranks, uint32_t streams)
+{
+    const size_t frame = (size_t)width * height;
+    for (uint32_t y = blockIdx.y; y < height; y += gridDim.y) {
+        if (((y >> 4) % nranks) != rank) continue;
+        for (uint32_t x = blockIdx.x * 256 + threadIdx.x; x < width; x += gridDim.x * 256) {
+            const size_t p = (size_t)y * width + x;
+            float4 v = accx[p];
+            for (uint32_t k = 1; k < streams; k++) {
+                float4 a = accx[(size_t)k * frame + p];
+                v.x = v.x + a.x; v.y = v.y + a.y; v.z = v.z + a.z; v.w = v.w + a.w;
+            }
+            accum[p] = v;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void zero_unowned_kernel(float4* accum, uint32_t width, uint32_t height,
                                                            uint32_t rank, uint32_t nranks)
 {
@@ -1283,6 +1329,26 @@ constexpr int ShadeMinWaves()
     return MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MINW
          : (MATS & PT_MATS_OPENPBR) ? PT_SHADE_OPENPBR_MINW : PT_SHADE_OTHER_MINW;
 }
+// A completed path (basic_scatter.glsl:344-359): its Sample accumulated into
+// the pixel (alpha counts the sample) and a new camera path generated with
+// the slot's RNG continuing from Scatter's draws.
+PT_DEV void CompletePath(const dscene& S, const dslots& L, const dframe& F, const dparams& Pm, rng& G, uint32_t s,
+                         uint32_t x, uint32_t y, uint32_t stream, pt3 Sample, bool act_none, pt3& O, pt3& V)
+{
+    float4* A = &StreamAccum(F, stream)[(size_t)y * F.width + x];
+    float4 Val = make_float4(Sample.x, Sample.y, Sample.z, 1.0f);
+    if (Pm.render_flags & PT_RENDER_FLAG_ACCUMULATE) {
+        float4 Old = *A;
+        Val.x = Val.x + Old.x; Val.y = Val.y + Old.y; Val.z = Val.z + Old.z; Val.w = Val.w + Old.w;
+    }
+    *A = Val;
+    GenerateNewPath(S, L, F, Pm, G, s, x, y, O, V, act_none);
+}
+
+#ifndef PT_SHADE_COMPACT
+#define PT_SHADE_COMPACT 0
+#endif
+
 // One tile of shade (basic_scatter.glsl:main for the tile's 256 slots).
 template <uint32_t MATS>
 PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const dparams& Pm, uint32_t tile)
@@ -1305,14 +1371,19 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
     const uint32_t s = base | threadIdx.x;
     const uint32_t p16 = L.pos[s];
 #endif
-    uint32_t x, y;
-    bool valid = SlotPixel(F, s, x, y);
+    uint32_t x, y, stream;
+    bool valid = SlotPixel(F, s, x, y, stream);
     pt3 O = v3s(0), V = v3s(0);
     bool completed = false;
+#if PT_SHADE_COMPACT
+    uint32_t cstate = 0;
+    pt3 csample = v3s(0.0f);
+    bool cactnone = false;
+#endif
     if (valid) {
         ShadeMark(SM_ENTRY);
         rng G;
-        G.State = pt_seed(x, y, Pm.seed);
+        G.State = pt_seed(x, y, StreamSeed(Pm.seed, stream));
 
         // LoadPath (basic.glsl.inc:159-198)
         path P;
@@ -1354,7 +1425,7 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
 #endif
             float2 c = L.uv[q];
             pt3 N, TX;
-            HitAttributesRecord(S, HitShape, h, c, HitMaterial, N, TX, UV, S.shape_uv[HitShape] != 0);
+            HitAttributesRecord(S, HitShape, h, c, HitMaterial, N, TX, UV, /*uv_if_textured=*/true);
             HitMaterial &= 0xFFFFu;
             HitShape &= 0xFFFFu;
             HitTime = h.x;
@@ -1373,21 +1444,65 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
             if ((na.x != act.x) | (na.y != act.y)) L.act[s] = na;
         } else {
             ShadeMark(SM_COMPLETED);
-            float4* A = &F.accum[(size_t)y * F.width + x];
-            float4 Val = make_float4(P.Sample.x, P.Sample.y, P.Sample.z, 1.0f);
-            if (Pm.render_flags & PT_RENDER_FLAG_ACCUMULATE) {
-                float4 Old = *A;
-                Val.x = Val.x + Old.x; Val.y = Val.y + Old.y; Val.z = Val.z + Old.z; Val.w = Val.w + Old.w;
-            }
-            *A = Val;
             completed = true;
-            GenerateNewPath(S, L, F, Pm, G, s, x, y, O, V, (act.x & act.y) == 0xFFFFFFFFu);
+#if PT_SHADE_COMPACT
+            cstate = G.State;
+            csample = P.Sample;
+            cactnone = (act.x & act.y) == 0xFFFFFFFFu;
+#else
+            CompletePath(S, L, F, Pm, G, s, x, y, stream, P.Sample, (act.x & act.y) == 0xFFFFFFFFu, O, V);
+#endif
         }
     }
     // Completed paths per wave (ptGetStats): one counter word per 64 slots,
     // updated by the wave's first lane (no atomics: a wave owns its word).
     uint64_t cm = __ballot(completed);
     if ((threadIdx.x & 63u) == 0) L.done[(base | threadIdx.x) >> 6] += (uint32_t)__popcll(cm);
+#if PT_SHADE_COMPACT
+    // Completion queue: the tile's completed paths (scattered over its waves
+    // by the hit / miss / roulette outcomes) are accumulated and restarted by
+    // the first threads of the block, so the camera-ray generation runs in
+    // full waves; the new rays come back through LDS to their slots' threads.
+    {
+        __shared__ uint32_t cq_slot[256], cq_rng[256], cq_count[4];
+        __shared__ float cq_f[6][256];
+        const uint32_t w = threadIdx.x >> 6;
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+        if ((threadIdx.x & 63u) == 0) cq_count[w] = (uint32_t)__popcll(cm);
+        __syncthreads();
+        uint32_t qi = below, total = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t c = cq_count[k];
+            qi += k < w ? c : 0u;
+            total += c;
+        }
+        if (completed) {
+            cq_slot[qi] = (s & 255u) | (cactnone ? 256u : 0u);
+            cq_rng[qi] = cstate;
+            cq_f[0][qi] = csample.x; cq_f[1][qi] = csample.y; cq_f[2][qi] = csample.z;
+        }
+        __syncthreads();
+        if (threadIdx.x < total) {
+            const uint32_t e = cq_slot[threadIdx.x];
+            const uint32_t s2 = base | (e & 255u);
+            uint32_t x2, y2, stream2;
+            (void)SlotPixel(F, s2, x2, y2, stream2);
+            rng G2;
+            G2.State = cq_rng[threadIdx.x];
+            pt3 O2, V2;
+            CompletePath(S, L, F, Pm, G2, s2, x2, y2, stream2,
+                         v3(cq_f[0][threadIdx.x], cq_f[1][threadIdx.x], cq_f[2][threadIdx.x]), (e & 256u) != 0, O2, V2);
+            cq_f[0][threadIdx.x] = O2.x; cq_f[1][threadIdx.x] = O2.y; cq_f[2][threadIdx.x] = O2.z;
+            cq_f[3][threadIdx.x] = V2.x; cq_f[4][threadIdx.x] = V2.y; cq_f[5][threadIdx.x] = V2.z;
+        }
+        __syncthreads();
+        if (completed) {
+            O = v3(cq_f[0][qi], cq_f[1][qi], cq_f[2][qi]);
+            V = v3(cq_f[3][qi], cq_f[4][qi], cq_f[5][qi]);
+        }
+    }
+#endif
     TileOrderStoreRay(L, s, valid, O, V, p16 >> 8);
 }
 
@@ -1606,6 +1721,15 @@ hipError_t pt_launch_atlas_tile(const float4* src, float4* dst, uint32_t w, uint
     uint64_t blocks = (texels + 255) / 256;
     hipLaunchKernelGGL(ptd::atlas_tile_kernel, dim3((uint32_t)(blocks < 65536 ? blocks : 65536)), dim3(256), 0, st, src,
                        dst, w, h, texels);
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_merge_streams(float4* accum, float4* accx, uint32_t width, uint32_t height, uint32_t rank,
+                                   uint32_t nranks, uint32_t streams, hipStream_t st)
+{
+    if (streams <= 1 || width == 0 || height == 0) return hipSuccess;
+    hipLaunchKernelGGL(ptd::merge_streams_kernel, dim3(Blocks(width), height < 32768u ? height : 32768u), dim3(256), 0,
+                       st, accum, accx, width, height, rank, nranks, streams);
     return hipGetLastError();
 }
 

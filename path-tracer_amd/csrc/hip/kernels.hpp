@@ -42,6 +42,13 @@ struct dframe {
     uint32_t tiles_x;
     uint32_t tiles_x_magic;   // ceil(2^32 / tiles_x): t / tiles_x = umulhi(t, magic)
                               // for t * tiles_x < 2^32 (checked at renderer creation)
+    // Path streams (ptCreateBasicRendererStreams): the renderer's tiles are
+    // `streams` copies of its owned tiles, stream k's seeds offset by k << 24
+    // and its paths accumulated in accx[k] (one stream: in accum itself).
+    uint32_t streams;         // 1: one path per owned pixel
+    uint32_t stream_tiles;    // tiles per stream
+    uint32_t stream_magic;    // ceil(2^32 / stream_tiles) (streams > 1)
+    float4* accx;             // streams x width x height (streams > 1)
 };
 
 struct dparams {
@@ -101,6 +108,9 @@ bool pt_rounds_available(const ptd::dslots& L);
 // (b % nranks != rank) before a frame-end reduce.
 hipError_t pt_launch_zero_unowned(float4* accum, uint32_t width, uint32_t height, uint32_t rank, uint32_t nranks,
                                   hipStream_t st);
+// Path streams' merge into the sample buffer's accumulator (owned bands).
+hipError_t pt_launch_merge_streams(float4* accum, float4* accx, uint32_t width, uint32_t height, uint32_t rank,
+                                   uint32_t nranks, uint32_t streams, hipStream_t st);
 // Packed row-major atlas (w x h texels per layer) -> AtlasIndex block layout;
 // needs w % 4 == 0 and h % 2 == 0.
 hipError_t pt_launch_atlas_tile(const float4* src, float4* dst, uint32_t w, uint32_t h, uint32_t layers, hipStream_t st);

@@ -105,8 +105,7 @@ struct pt_scene {
     ptd::dscene d{};
     dbuf<pt_packed_texture> textures;
     dbuf<uint32_t> material;
-    dbuf<pt_packed_shape> shapes;
-    dbuf<uint8_t> shape_uv;              // per shape: its material reads texture coordinates
+    dbuf<pt_packed_shape> shapes;        // device copy: Pad0 = PT_SHAPE_FLAG_UV when the material reads UVs
     dbuf<pt_packed_shape_node> shape_nodes;
     dbuf<pt_packed_mesh_face> faces;
     dbuf<pt_packed_mesh_vertex> vertices;
@@ -173,7 +172,11 @@ struct pt_basic_renderer {
     int fused = 1;                      // fused rounds mode (ptSetBasicRendererFusedRounds)
     int openpbr = 0;                    // shade OpenPBR materials (ptSetBasicRendererOpenPBR)
     uint32_t round_batch = 0;           // rounds per launch of consecutive Run(1) rounds (0: automatic)
-    uint64_t pixels = 0;                // image pixels owned (valid slots)
+    uint64_t pixels = 0;                // image pixels owned
+    uint32_t streams = 1;               // path streams per owned pixel (ptCreateBasicRendererStreams)
+    uint32_t stream_tiles = 0;          // tiles per stream
+    uint64_t valid_slots = 0;           // streams x pixels: the paths of one round
+    dbuf<float4> accx;                  // streams > 1: each stream's accumulator (streams x width x height)
     uint64_t rays = 0;                  // rays traced since the last Reset
     dbuf<uint32_t> spill;
 };
@@ -411,6 +414,10 @@ ptd::dframe Frame(pt_basic_renderer* r)
     F.nranks = r->nranks;
     F.tiles_x = r->tiles_x;
     F.tiles_x_magic = r->tiles_x > 1 ? (uint32_t)(((1ull << 32) + r->tiles_x - 1) / r->tiles_x) : 0u;
+    F.streams = r->streams;
+    F.stream_tiles = r->stream_tiles;
+    F.stream_magic = r->streams > 1 ? (uint32_t)(((1ull << 32) + r->stream_tiles - 1) / r->stream_tiles) : 0u;
+    F.accx = r->accx.ptr;
     return F;
 }
 
@@ -513,7 +520,7 @@ void ptDestroyScene(pt_device* d, pt_scene* s)
 {
     if (!s) return;
     if (d) (void)hipSetDevice(d->id);
-    s->textures.release(); s->material.release(); s->shapes.release(); s->shape_uv.release(); s->shape_nodes.release();
+    s->textures.release(); s->material.release(); s->shapes.release(); s->shape_nodes.release();
     s->faces.release(); s->vertices.release(); s->vertex_attr.release(); s->vertex_v.release(); s->mesh_nodes.release(); s->cameras.release(); s->atlas.release();
     delete s;
 }
@@ -656,14 +663,13 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
         }
     }
     if (first || (dirty & PT_SCENE_DIRTY_MATERIALS)) PT_HIP(s->material.upload(p->material_data, p->material_word_count));
-    if (first || (dirty & PT_SCENE_DIRTY_SHAPES)) {
-        PT_HIP(s->shapes.upload(p->shapes, p->shape_count));
-        PT_HIP(s->shape_nodes.upload(p->shape_nodes, p->shape_node_count));
-    }
+    if (first || (dirty & PT_SCENE_DIRTY_SHAPES)) PT_HIP(s->shape_nodes.upload(p->shape_nodes, p->shape_node_count));
     if (first || (dirty & (PT_SCENE_DIRTY_SHAPES | PT_SCENE_DIRTY_MATERIALS))) {
-        std::vector<uint8_t> uv(p->shape_count);
-        for (uint32_t i = 0; i < p->shape_count; i++) uv[i] = MaterialReadsUV(p, p->shapes[i].MaterialIndex) ? 1 : 0;
-        PT_HIP(s->shape_uv.upload(uv.data(), uv.size()));
+        // The device's shape records carry, in their unused Pad0 word, whether
+        // the shape's material reads texture coordinates (HitAttributesV).
+        std::vector<pt_packed_shape> sh(p->shapes, p->shapes + p->shape_count);
+        for (pt_packed_shape& S : sh) S.Pad0 = MaterialReadsUV(p, S.MaterialIndex) ? ptd::PT_SHAPE_FLAG_UV : 0u;
+        PT_HIP(s->shapes.upload(sh.data(), sh.size()));
     }
     if (first || (dirty & PT_SCENE_DIRTY_MESHES)) {
         // Device face records carry {Position0, Edge1, Edge2} (traverse.hpp
@@ -697,7 +703,6 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     D.textures = s->textures.ptr;
     D.material = s->material.ptr;
     D.shapes = s->shapes.ptr;
-    D.shape_uv = s->shape_uv.ptr;
     D.shape_nodes = reinterpret_cast<const float4*>(s->shape_nodes.ptr);
     D.mesh_faces = reinterpret_cast<const float4*>(s->faces.ptr);
     D.mesh_vertices = reinterpret_cast<const uint2*>(s->vertices.ptr);
@@ -826,11 +831,12 @@ int ptReadResolvedImageSRGB8(pt_device* d, pt_sample_buffer* b, uint8_t* rgba8)
 // C3 -2.4 %: DESIGN.md §4).
 constexpr uint32_t TILE_ORDER_PERIOD = 16;
 
-pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, pt_sample_buffer* b, uint32_t rank,
-                                                    uint32_t nranks)
+pt_basic_renderer* ptCreateBasicRendererStreams(pt_device* d, pt_scene* s, pt_sample_buffer* b, uint32_t rank,
+                                                uint32_t nranks, uint32_t streams)
 {
     if (!d || !s || !b) { SetError("null argument"); return nullptr; }
     if (nranks == 0 || rank >= nranks) { SetError("bad partition %u/%u", rank, nranks); return nullptr; }
+    if (streams == 0 || streams > 256) { SetError("bad stream count %u (1..256)", streams); return nullptr; }
     if (hipSetDevice(d->id) != hipSuccess) { SetError("hipSetDevice failed"); return nullptr; }
     pt_basic_renderer* r = new pt_basic_renderer;
     r->dev = d;
@@ -841,10 +847,15 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     r->tiles_x = (b->width + 15) / 16;
     uint32_t bands = (b->height + 15) / 16;
     uint32_t owned = bands > rank ? (bands - rank + nranks - 1) / nranks : 0;
-    uint64_t n = (uint64_t)owned * r->tiles_x * 256;
-    // TileRow's reciprocal division is exact while every tile index t has
-    // t * tiles_x < 2^32.
-    if ((uint64_t)owned * r->tiles_x * r->tiles_x >= (1ull << 32)) { SetError("frame too large"); delete r; return nullptr; }
+    const uint64_t T = (uint64_t)owned * r->tiles_x;   // tiles per stream
+    uint64_t n = T * streams * 256;
+    // TileRow's and TileStream's reciprocal divisions are exact while every
+    // tile index t has t * divisor < 2^32.
+    if (T * r->tiles_x >= (1ull << 32) || (streams > 1 && T * T * streams >= (1ull << 32))) {
+        SetError("frame too large");
+        delete r;
+        return nullptr;
+    }
     if (n > 0xFFFFFFFFull / 2) { SetError("too many slots"); delete r; return nullptr; }
     uint32_t ns = (uint32_t)n;
     bool ok = r->ray.alloc(ns) == hipSuccess && r->hit.alloc(ns) == hipSuccess && r->thr.alloc(ns) == hipSuccess &&
@@ -853,6 +864,10 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
               r->outcome.alloc((size_t)(ns / 256) * 4 * ptd::PT_OUTCOME_CLASSES + 1) == hipSuccess &&
               r->tilecost.alloc((size_t)(ns / 256) * 4 + 1) == hipSuccess && r->order.alloc(ns / 256 + 1) == hipSuccess &&
               r->done.alloc(ns / 64 + 1) == hipSuccess;
+    const size_t frame_px = (size_t)b->width * b->height;
+    if (ok && streams > 1)
+        ok = r->accx.alloc((size_t)streams * frame_px) == hipSuccess &&
+             hipMemset(r->accx.ptr, 0, (size_t)streams * frame_px * 16) == hipSuccess;
     if (ok && ns) {
         ok = hipMemset(r->ray.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->hit.ptr, 0, (size_t)ns * 16) == hipSuccess &&
              hipMemset(r->thr.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->prob.ptr, 0, (size_t)ns * 16) == hipSuccess &&
@@ -874,10 +889,12 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
         SetError("renderer slot allocation failed (%u slots)", ns);
         r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->lam.release(); r->uv.release(); r->act.release();
         r->pos.release(); r->slotof.release(); r->outcome.release(); r->tilecost.release(); r->order.release();
-        r->done.release();
+        r->done.release(); r->accx.release();
         delete r;
         return nullptr;
     }
+    r->streams = streams;
+    r->stream_tiles = (uint32_t)T;
     r->slots.ray = r->ray.ptr;
     r->slots.hit = r->hit.ptr;
     r->slots.uv = r->uv.ptr;
@@ -896,10 +913,32 @@ pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, p
     r->slots.tile_count = ns / 256;
     for (uint32_t band = rank; band < bands; band += nranks)
         r->pixels += (uint64_t)b->width * std::min<uint32_t>(16u, b->height - band * 16u);
+    r->valid_slots = r->pixels * streams;
     b->rank = rank;
     b->nranks = nranks;
     return r;
 }
+
+pt_basic_renderer* ptCreateBasicRendererPartitioned(pt_device* d, pt_scene* s, pt_sample_buffer* b, uint32_t rank,
+                                                    uint32_t nranks)
+{
+    return ptCreateBasicRendererStreams(d, s, b, rank, nranks, 1);
+}
+
+// The sample buffer's owned pixels := the streams' accumulators summed in
+// stream order, ((A0 + A1) + A2) ...; the streams keep accumulating, so a
+// later merge gives the new totals.
+int ptMergeBasicRendererStreams(pt_device* d, pt_basic_renderer* r)
+{
+    if (!d || !r || !r->buffer) { SetError("null argument"); return -1; }
+    if (r->streams == 1) return 0;
+    PT_HIP(hipSetDevice(d->id));
+    PT_HIP(pt_launch_merge_streams(r->buffer->accum, r->accx.ptr, r->buffer->width, r->buffer->height, r->rank,
+                                   r->nranks, r->streams, d->stream));
+    return 0;
+}
+
+uint32_t ptBasicRendererStreams(pt_basic_renderer* r) { return r ? r->streams : 0; }
 
 pt_basic_renderer* ptCreateBasicRenderer(pt_device* d, pt_scene* s, pt_sample_buffer* b)
 {
@@ -915,6 +954,7 @@ void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
     r->tilecost.release(); r->order.release();
     r->done.release();
     r->spill.release();
+    r->accx.release();
     delete r;
 }
 
@@ -993,7 +1033,7 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
             if (int e = EndTimed(d, ep)) return e;
         }
         if (sort) PT_HIP(pt_launch_tile_order(L, d->stream));
-        r->rays += r->pixels;
+        r->rays += r->valid_slots;
     }
     return 0;
 }
@@ -1033,7 +1073,7 @@ static int RunRounds(pt_device* d, pt_basic_renderer* r, uint64_t k)
                 if (int e = EndTimed(d, ep)) return e;
                 // The batch's block times order the next batch.
                 if (r->slots.order) PT_HIP(pt_launch_tile_order(r->slots, d->stream));
-                r->rays += r->pixels * n;
+                r->rays += r->valid_slots * n;
                 k -= n;
             }
             return 0;
@@ -1100,8 +1140,8 @@ int ptGetStats(pt_device* d, pt_basic_renderer* r, uint64_t* rays, uint64_t* sam
 // The completed count is read back between batches of rounds: a batch is
 // never longer than the rounds that could not reach the target even if every
 // slot completed a path each round, or than 90 % of the rounds the last
-// batch's completion rate predicts -- so the frame ends at (or, if the rate
-// jumps by > 10 % within a batch, a few rounds after) the reference's round.
+// batch's completion rate predicts, and within the last 16 predicted rounds
+// only the former -- so the frame ends at the reference's round.
 int ptRenderFrame(pt_device* d, pt_basic_renderer* r, uint64_t target_samples, uint32_t max_rounds,
                   uint32_t* rounds_out, uint64_t* samples_out)
 {
@@ -1112,7 +1152,7 @@ int ptRenderFrame(pt_device* d, pt_basic_renderer* r, uint64_t target_samples, u
     uint32_t rounds = 2;
     uint64_t samples = 0, prev = 0;
     uint32_t last_batch = 0;
-    const uint64_t px = std::max<uint64_t>(r->pixels, 1);
+    const uint64_t px = std::max<uint64_t>(r->valid_slots, 1);   // paths one round can complete
     for (;;) {
         if (int e = ptGetStats(d, r, nullptr, &samples)) return e;
         if (samples >= target_samples || rounds >= max_rounds) break;
@@ -1120,7 +1160,12 @@ int ptRenderFrame(pt_device* d, pt_basic_renderer* r, uint64_t target_samples, u
         uint64_t k = (remaining + px - 1) / px;                      // cannot overshoot
         if (last_batch > 0 && samples > prev) {
             double rate = (double)(samples - prev) / last_batch;     // completions per round
-            k = std::max<uint64_t>(k, (uint64_t)(0.9 * (double)remaining / rate));
+            // 90 % of the rounds the last batch's rate predicts; within the
+            // last 16 predicted rounds only the rounds that cannot overshoot,
+            // so a rate that rises near the end cannot carry the frame past
+            // the round that first reaches the target.
+            const uint64_t kr = (uint64_t)(0.9 * (double)remaining / rate);
+            if (kr >= 16) k = std::max<uint64_t>(k, kr);
         }
         k = std::max<uint64_t>(1, std::min<uint64_t>(k, max_rounds - rounds));
         if (int e = RunRounds(d, r, k)) return e;
@@ -1133,9 +1178,10 @@ int ptRenderFrame(pt_device* d, pt_basic_renderer* r, uint64_t target_samples, u
     return 0;
 }
 
-int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state* out)
+int ptReadBasicRendererStreamState(pt_device* d, pt_basic_renderer* r, uint32_t stream, pt_pixel_state* out)
 {
     if (!d || !r || !out) { SetError("null argument"); return -1; }
+    if (stream >= r->streams) { SetError("stream %u >= the renderer's %u streams", stream, r->streams); return -1; }
     PT_HIP(hipSetDevice(d->id));
     PT_WAIT(d);
     uint32_t n = r->slots.n;
@@ -1167,13 +1213,13 @@ int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state*
     PT_HIP(hipMemcpy(pos.data(), r->pos.ptr, (size_t)n * 2, hipMemcpyDeviceToHost));
     uint32_t W = r->buffer->width, H = r->buffer->height;
     auto bits = [](float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; };
-    for (uint32_t s = 0; s < n; s++) {
-        uint32_t t = s >> 8, l = s & 255u, k = t / r->tiles_x, tx = t - k * r->tiles_x;
+    const uint32_t s0 = stream * r->stream_tiles * 256, s1 = s0 + r->stream_tiles * 256;
+    for (uint32_t s = s0; s < s1; s++) {
+        uint32_t t = (s >> 8) - stream * r->stream_tiles, l = s & 255u, k = t / r->tiles_x, tx = t - k * r->tiles_x;
         uint32_t x = tx * 16 + (l & 15u), y = (r->rank + k * r->nranks) * 16 + (l >> 4);
         if (x >= W || y >= H) continue;
         pt_pixel_state& O = out[(size_t)y * W + x];
-        // Ray and hit records live at the slot's TileOrder positions (global
-        // sort: both by slot).
+        // Ray and hit records live at the slot's TileOrder positions.
         uint32_t qr = (s & ~255u) | (pos[s] >> 8u), qh = (s & ~255u) | (pos[s] & 255u);
         O.origin[0] = ray[qr].x; O.origin[1] = ray[qr].y; O.origin[2] = ray[qr].z;
         O.packed_velocity = bits(ray[qr].w);
@@ -1191,6 +1237,11 @@ int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state*
         O.active23 = act[s].y;
     }
     return 0;
+}
+
+int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state* out)
+{
+    return ptReadBasicRendererStreamState(d, r, 0, out);
 }
 
 pt_preview* ptCreatePreviewRenderContext(pt_device* d, pt_scene* s)

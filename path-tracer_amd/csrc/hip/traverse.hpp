@@ -595,11 +595,13 @@ PT_DEV float4 CompactHit(const lane_state& Ln, bool vidx21)
 
 // Hit attribute reconstruction (scene.glsl.inc:535-608).  Mesh faces: the
 // vertex indices come packed in the hit record (vidx21) or from the face.
-// uv = false: the caller never reads the texture coordinates (the hit
-// shape's material samples no texture, dscene::shape_uv), which are then left
-// 0 instead of computed (a sphere's atan2, a mesh's three vertex V loads).
+// uv_if_textured: the caller reads the texture coordinates only through the
+// hit material's textures (shade), so hits on shapes whose material samples
+// none (the device shape record's PT_SHAPE_FLAG_UV, loaded with its type)
+// leave them 0 instead of computing them (a sphere's atan2, a mesh's three
+// vertex V loads).
 PT_DEV void HitAttributesV(const dscene& S, uint32_t ShapeIndex, bool packed, uint32_t Z, uint32_t Wd, pt3 C,
-                           uint32_t& Material, pt3& Normal, pt3& TangentX, pt2& UV, bool uv = true);
+                           uint32_t& Material, pt3& Normal, pt3& TangentX, pt2& UV, bool uv_if_textured = false);
 
 PT_DEV void HitAttributes(const dscene& S, uint32_t ShapeIndex, uint32_t Prim, pt3 C, uint32_t& Material, pt3& Normal,
                           pt3& TangentX, pt2& UV)
@@ -609,25 +611,30 @@ PT_DEV void HitAttributes(const dscene& S, uint32_t ShapeIndex, uint32_t Prim, p
 
 // From a compact hit record (h = {Time, Shape, z, w}, c = {C.y, C.z}).
 PT_DEV void HitAttributesRecord(const dscene& S, uint32_t ShapeIndex, float4 h, float2 c, uint32_t& Material,
-                                pt3& Normal, pt3& TangentX, pt2& UV, bool uv = true)
+                                pt3& Normal, pt3& TangentX, pt2& UV, bool uv_if_textured = false)
 {
     const bool mesh = S.shapes[ShapeIndex].Type == PT_SHAPE_TYPE_MESH_INSTANCE;
     if (S.vidx21) {
         pt3 C = mesh ? v3(1 - c.x - c.y, c.x, c.y) : v3(h.z, c.x, c.y);
         HitAttributesV(S, ShapeIndex, true, __float_as_uint(h.z), __float_as_uint(h.w), C, Material, Normal, TangentX, UV,
-                       uv);
+                       uv_if_textured);
     } else {
         HitAttributesV(S, ShapeIndex, false, __float_as_uint(h.z), 0u, v3(h.w, c.x, c.y), Material, Normal, TangentX, UV,
-                       uv);
+                       uv_if_textured);
     }
 }
 
 PT_DEV void HitAttributesV(const dscene& S, uint32_t ShapeIndex, bool packed, uint32_t Z, uint32_t Wd, pt3 C,
-                           uint32_t& Material, pt3& Normal, pt3& TangentX, pt2& UV, bool uv)
+                           uint32_t& Material, pt3& Normal, pt3& TangentX, pt2& UV, bool uv_if_textured)
 {
     UV = v2(0.0f, 0.0f);
     const pt_packed_shape* Shape = &S.shapes[ShapeIndex];
     Material = Shape->MaterialIndex;
+#if PT_EXP_UV_ALWAYS
+    const bool uv = true;
+#else
+    const bool uv = !uv_if_textured || (Shape->Pad0 & PT_SHAPE_FLAG_UV);
+#endif
     int32_t Type = Shape->Type;
     const float* To = Shape->Transform.To;
     const float* From = Shape->Transform.From;

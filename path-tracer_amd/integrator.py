@@ -222,11 +222,16 @@ class BasicRenderer:
 
     _FIELDS = ("FrameIndex", "CameraIndex", "RenderFlags", "PathLengthLimit", "PathTerminationProbability")
 
-    def __init__(self, device: Device, scene: DeviceScene, sample_buffer: SampleBuffer, rank: int = 0, nranks: int = 1):
+    def __init__(self, device: Device, scene: DeviceScene, sample_buffer: SampleBuffer, rank: int = 0, nranks: int = 1,
+                 streams: int = 1):
+        """rank / nranks: the 16-row pixel bands owned (b % nranks == rank);
+        streams: independent paths per owned pixel, stream k seeded at
+        FrameIndex + (k << 24) (ptCreateBasicRendererStreams)."""
         L = N.hip_lib()
         self.device, self.scene, self.sample_buffer = device, scene, sample_buffer
-        self.rank, self.nranks = rank, nranks
-        self._h = L.ptCreateBasicRendererPartitioned(device.handle, scene.handle, sample_buffer.handle, rank, nranks)
+        self.rank, self.nranks, self.streams = rank, nranks, streams
+        self._h = L.ptCreateBasicRendererStreams(device.handle, scene.handle, sample_buffer.handle, rank, nranks,
+                                                 streams)
         if not self._h:
             raise PathTracerError(L.ptGetLastError().decode())
         self._params = L.ptBasicRendererParams(self._h)
@@ -249,6 +254,11 @@ class BasicRenderer:
     @property
     def slot_count(self) -> int:
         return int(N.hip_lib().ptBasicRendererSlotCount(self._h))
+
+    def merge_streams(self):
+        """Add streams 1.. into the sample buffer (stream order) and clear
+        them (ptMergeBasicRendererStreams); a no-op for one stream."""
+        _check(N.hip_lib().ptMergeBasicRendererStreams(self.device.handle, self._h), "ptMergeBasicRendererStreams")
 
     def set_fused_rounds(self, mode: int):
         """0 never / 1 automatic / 2 whenever possible (ptSetBasicRendererFusedRounds)."""
@@ -309,7 +319,7 @@ class BasicRenderer:
         sb = self.sample_buffer
         tiles_x, bands = (sb.width + 15) // 16, (sb.height + 15) // 16
         owned = (bands - self.rank + self.nranks - 1) // self.nranks if bands > self.rank else 0
-        return owned * tiles_x * 256
+        return owned * tiles_x * 256 * self.streams
 
     def extend_step_counts(self) -> np.ndarray:
         """Traversal steps of every current ray, per ray position (diagnostic)."""
@@ -317,11 +327,12 @@ class BasicRenderer:
         _check(N.hip_lib().ptExtendStepCounts(self.device.handle, self._h, out.ctypes.data), "ptExtendStepCounts")
         return out
 
-    def read_state(self) -> np.ndarray:
+    def read_state(self, stream: int = 0) -> np.ndarray:
+        """Per-pixel state of one path stream, image order (owned pixels)."""
         sb = self.sample_buffer
         out = np.zeros(sb.width * sb.height, dtype=N.PIXEL_STATE_DTYPE)
-        _check(N.hip_lib().ptReadBasicRendererState(self.device.handle, self._h, out.ctypes.data),
-               "ptReadBasicRendererState")
+        _check(N.hip_lib().ptReadBasicRendererStreamState(self.device.handle, self._h, int(stream), out.ctypes.data),
+               "ptReadBasicRendererStreamState")
         return out.reshape(sb.height, sb.width)
 
     def close(self):

@@ -28,7 +28,7 @@ def load(path):
 
 
 def short(name):
-    for k in ("extend", "shade", "raygen", "finalize", "round"):
+    for k in ("extend", "shade", "raygen", "finalize", "rounds", "round"):
         if f"{k}_kernel" in name:
             return k
     return name[:40]

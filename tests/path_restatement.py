@@ -85,8 +85,11 @@ def _fract(x):
 
 
 def _normalize(v):
-    r = f32(1.0) / np.sqrt((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2])
-    return [v[0] * r, v[1] * r, v[2] * r]
+    # GLSL normalize of a zero vector is inf * 0 = NaN in IEEE float32 (the
+    # OpenPBR sampler reaches it); the arithmetic is the restated behaviour.
+    with np.errstate(divide="ignore", invalid="ignore"):
+        r = f32(1.0) / np.sqrt((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2])
+        return [v[0] * r, v[1] * r, v[2] * r]
 
 
 def _safe_normalize(v):

@@ -62,6 +62,11 @@ def tone_map(color, mode, white):
 
 
 def encode_srgb8(c):
+    """B8G8R8A8_SRGB store of a float channel.  Vulkan's UNORM conversion
+    takes NaN to 0 (the device's and the oracle's pt_clamp does so by
+    min/max), so NaN is mapped to 0 here by rule, not left to numpy's
+    platform-defined float -> uint8 cast."""
+    c = np.where(np.isnan(c), f32(0.0), c).astype(f32)
     c = np.clip(c, f32(0.0), f32(1.0))
     powed = _fp_vec("exp", _fp_vec("log", c) * (f32(1.0) / f32(2.4)))
     e = np.where(c <= f32(0.0031308), f32(12.92) * c, f32(1.055) * powed - f32(0.055)).astype(f32)
@@ -69,7 +74,16 @@ def encode_srgb8(c):
 
 
 def resolve(accum, brightness=1.0, mode=CLAMP, white=1.0):
-    """(OutColor float32 (..., 4), sRGB8 bytes (..., 4)) of accumulator pixels."""
+    """(OutColor float32 (..., 4), sRGB8 bytes (..., 4)) of accumulator pixels.
+    IEEE float32 semantics throughout: inf / NaN arithmetic is the restated
+    behaviour (e.g. Reinhard on black pixels), so numpy's warnings for it are
+    silenced; the one platform-defined step, NaN -> uint8, is ruled out in
+    encode_srgb8."""
+    with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
+        return _resolve(accum, brightness, mode, white)
+
+
+def _resolve(accum, brightness, mode, white):
     a = np.asarray(accum, f32).reshape(-1, 4)
     color = np.zeros((len(a), 3), f32)
     live = a[:, 3] > 0

@@ -70,6 +70,61 @@ def test_c4_rank_of_8_partition_bit_exact(pt, dev, rank):
     s.close()
 
 
+@pytest.mark.parametrize("config,rank,streams", [(4, 0, 2), (4, 7, 2), (3, 5, 8)])
+def test_band_path_streams_bit_exact(pt, dev, config, rank, streams):
+    """Path streams: a rank-of-8 band partition carrying
+    `streams` paths per owned pixel.  Every stream's slot state equals the
+    oracle's one-stream render of the same bands started at FrameIndex
+    k << 24, and after ptMergeBasicRendererStreams the sample buffer holds the
+    streams' accumulators summed in stream order, bit for bit; a merge after
+    more rounds gives the new totals the same way.  C4
+    at full size (ranks 0 and 7, two streams: 2.09 M slots per launch), C3
+    rank 5 of 8 with eight streams (2.2 M slots)."""
+    s = pt.Scene.config(config)
+    W, H = s.info.width, s.info.height
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    sb = pt.SampleBuffer(dev, W, H)
+    r = pt.BasicRenderer(dev, ds, sb, rank=rank, nranks=8, streams=streams)
+    bands = len(range(rank, (H + 15) // 16, 8))
+    assert r.slot_count == streams * bands * ((W + 15) // 16) * 256
+    r.RenderFlags = 3
+    r.reset()
+    r.run(2)
+    r.run(1)
+    r.merge_streams()
+    dev.synchronize()
+    got1 = sb.read()
+    states = [r.read_state(k) for k in range(streams)]
+    r.run(1)
+    r.merge_streams()
+    dev.synchronize()
+    got2 = sb.read()
+    owned = pt.owned_pixels(W, H, rank, 8)
+    want1 = np.zeros((H, W, 4), np.float32)
+    want2 = np.zeros((H, W, 4), np.float32)
+    for k in range(streams):
+        o = oracle_lib.OracleRenderer(s.packs(), W, H, rank=rank, nranks=8)
+        o.RenderFlags = 3
+        o.FrameIndex = k << 24
+        o.reset()
+        o.run(2)
+        o.run(1)
+        compare_state(states[k][owned], o.state()[owned])
+        want1 = want1 + o.accum()          # float32, stream order
+        o.run(1)
+        want2 = want2 + o.accum()
+        o.close()
+    assert np.array_equal(bits(got1[owned]), bits(want1[owned]))
+    assert np.array_equal(bits(got2[owned]), bits(want2[owned]))
+    assert got2[owned][:, 3].sum() == want2[owned][:, 3].sum() > 0
+    r2, samples = r.stats()
+    assert r2 == 4 * streams * int(owned.sum())           # every stream's slot traces a ray per round
+    for x in (r, sb, ds):
+        x.close()
+    s.close()
+
+
 # (config, W, H, RenderFlags, PathTerminationProbability)
 PARAM_CASES = [
     (1, 64, 64, 3, 0.1),     # roulette on, few terminations
@@ -666,8 +721,14 @@ def test_whole_1024spp_frame_bit_exact(pt, dev):
     o.RenderFlags = 3
     o.reset()
     o.run(2)
-    for _ in range(rounds - 2):
+    for _ in range(rounds - 3):
         o.run(1)
+    # The frame ends at the reference's round: one round earlier the target
+    # was not yet reached (the batches sized from the completion
+    # rate must not run past it).
+    _, before_last = o.counters()
+    assert before_last < target
+    o.run(1)
     _, osamples = o.counters()
     oa = o.accum()
     o.close()

@@ -54,5 +54,25 @@ def test_resolve_of_a_rendered_frame(pt):
     for mode in (rr.CLAMP, rr.REINHARD, rr.HABLE, rr.ACES):
         want, want8 = oracle_lib.resolve(acc, brightness=1.5, mode=mode, white=2.0)
         got, got8 = rr.resolve(acc, brightness=1.5, mode=mode, white=2.0)
+        assert np.array_equal(np.isnan(got), np.isnan(want))
         assert np.array_equal(np.nan_to_num(got).view(np.uint32), np.nan_to_num(want).view(np.uint32))
         assert np.array_equal(got8, want8)
+        # NaN channels (Reinhard's c * new / old on black pixels) store 0 by
+        # the UNORM rule in the oracle, as in the restatement.
+        nan = np.isnan(want[..., :3])
+        assert np.all(want8[..., :3][nan] == 0)
+
+
+def test_srgb8_store_of_nan_and_infinities(pt):
+    """The sRGB8 store's rule for non-finite channels, pinned on the oracle:
+    NaN -> 0, +inf -> 255, -inf -> 0 (UNORM conversion after the clamp)."""
+    a = np.zeros((4, 4), np.float32)
+    a[:, 3] = 1.0
+    a[0, :3] = np.nan
+    a[1, :3] = np.inf
+    a[2, :3] = -np.inf
+    a[3, :3] = [0.25, 0.5, 1.0]
+    want, want8 = oracle_lib.resolve(a, brightness=1.0, mode=rr.CLAMP, white=1.0)
+    got, got8 = rr.resolve(a, brightness=1.0, mode=rr.CLAMP, white=1.0)
+    assert np.array_equal(got8, want8)
+    assert np.all(want8[0, :3] == 0)

@@ -2,12 +2,14 @@
 
 For each config and N, renders the partition rank 0 of N gets (the 16-row
 bands b with b % N == 0: the most bands of any rank, so the slowest rank)
-on device 0 and times K rounds.  The predicted N-GPU throughput is the whole
-frame's rays per round / rank 0's round time.  This is a PREDICTION: the
+on device 0 and times K rounds.  The predicted N-GPU throughput is rank 0's
+ray rate scaled to the whole frame (rank 0 owns the most bands).  Band
+partitions carry path streams (bench.py's automatic count: about 2^21 slots
+per launch) unless --streams says otherwise.  This is a PREDICTION: the
 other ranks run on other GPUs in the real run, and the frame-end RCCL band
 gather (ptCommGatherSampleBuffer) is not included.
 
-usage: python tools/rehearse_scaling.py OUT.json [--steps K] [--configs 3,4] [--ns 1,2,4,8]
+usage: python tools/rehearse_scaling.py OUT.json [--steps K] [--configs 3,4] [--ns 1,2,4,8] [--streams auto|1,2,..]
 """
 from __future__ import annotations
 
@@ -22,6 +24,7 @@ from pathlib import Path
 import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
+FILL_SLOTS = 1 << 21      # as bench.py
 
 
 def load_package():
@@ -39,7 +42,7 @@ def main():
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--configs", default="3,4")
     ap.add_argument("--ns", default="1,2,4,8")
-    ap.add_argument("--groups", default="", help="comma list of PT_RUN_GROUPS values to try (default: the runtime's choice)")
+    ap.add_argument("--streams", default="auto", help="comma list of path stream counts, or auto (bench.py's choice)")
     ap.add_argument("--batches", default="0", help="comma list of round batches (ptSetBasicRendererRoundBatch) to try")
     args = ap.parse_args()
     pt = load_package()
@@ -50,15 +53,12 @@ def main():
         W, H = scene.info.width, scene.info.height
         ds = pt.DeviceScene(dev)
         ds.update(scene)
-        for n, groups, batch in [(int(x), g, int(b)) for x in args.ns.split(",")
-                                 for g in (args.groups.split(",") if args.groups else [None])
-                                 for b in args.batches.split(",")]:
-            if groups is None:
-                os.environ.pop("PT_RUN_GROUPS", None)
-            else:
-                os.environ["PT_RUN_GROUPS"] = groups
+        for n, st, batch in [(int(x), k, int(b)) for x in args.ns.split(",")
+                             for k in args.streams.split(",") for b in args.batches.split(",")]:
+            owned = int(np.sum(pt.owned_pixels(W, H, 0, n)))
+            streams = max(1, round(FILL_SLOTS / owned)) if st == "auto" else int(st)
             sb = pt.SampleBuffer(dev, W, H)
-            r = pt.BasicRenderer(dev, ds, sb, rank=0, nranks=n)
+            r = pt.BasicRenderer(dev, ds, sb, rank=0, nranks=n, streams=streams)
             r.RenderFlags = scene.info.render_flags
             r.set_round_batch(batch)
             r.reset()
@@ -77,20 +77,21 @@ def main():
             dev.synchronize()
             dt = time.perf_counter() - t0
             rays1, _ = r.stats()
-            ne, me = dev.kernel_stats(1)
-            ns_, ms = dev.kernel_stats(2)
-            nr, mr = dev.kernel_stats(5)
+            per_round = {}
+            for name, k in (("extend", 1), ("shade", 2), ("round", 5), ("rounds", 6)):
+                nk, mk = dev.kernel_stats(k)
+                if nk:
+                    per_round[name] = round(mk / max(dev.kernel_rounds(k), 1), 4)
             dev.set_profiling(False)
-            owned = int(np.sum(pt.owned_pixels(W, H, 0, n)))
             step_ms = dt / args.steps * 1e3
+            rate = (rays1 - rays0) / dt / 1e6
             row = {
-                "config": cfg, "frame": f"{W}x{H}", "n_gpus": n, "rank0_pixels": owned,
-                "rank0_tiles": r.slot_count // 256, "run_groups": r.run_groups, "round_batch": batch,
+                "config": cfg, "frame": f"{W}x{H}", "n_gpus": n, "rank0_pixels": owned, "streams": streams,
+                "rank0_slots": r.slot_count, "round_batch": batch,
                 "rank0_ms_per_step": round(step_ms, 4),
-                "rank0_mrays_per_s": round((rays1 - rays0) / dt / 1e6, 1),
-                "extend_ms": round(me / max(ne, 1), 4), "shade_ms": round(ms / max(ns_, 1), 4),
-                "round_launch_ms": round(mr / max(nr, 1), 4),   # fused round / round batch launch
-                "predicted_frame_mrays_per_s": round(W * H / (step_ms * 1e-3) / 1e6, 1),
+                "rank0_mrays_per_s": round(rate, 1),
+                "kernel_ms_per_round": per_round,
+                "predicted_frame_mrays_per_s": round(rate * W * H / owned, 1),
             }
             rows.append(row)
             print(json.dumps(row), flush=True)
@@ -100,7 +101,7 @@ def main():
         scene.close()
     base = {}
     for r in rows:
-        if r["n_gpus"] == 1:
+        if r["n_gpus"] == 1 and r["streams"] == 1:
             base[r["config"]] = max(base.get(r["config"], 0), r["predicted_frame_mrays_per_s"])
     for r in rows:
         b = base.get(r["config"])

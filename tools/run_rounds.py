@@ -18,6 +18,11 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--settle", type=int, default=34)
     ap.add_argument("--rounds", type=int, default=64)
+    ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--nranks", type=int, default=1)
+    ap.add_argument("--streams", type=int, default=1)
+    ap.add_argument("--fused", type=int, default=0, help="ptSetBasicRendererFusedRounds mode (0 never, 1 auto)")
+    ap.add_argument("--batch", type=int, default=1, help="round batch for the timed rounds (1: one launch pair each)")
     a = ap.parse_args()
     if a.lib:
         os.environ["PT_HIP_LIB"] = str((ROOT / a.lib) if not os.path.isabs(a.lib) else a.lib)
@@ -30,8 +35,9 @@ def main():
     ds = pt.DeviceScene(dev)
     ds.update(scene)
     sb = pt.SampleBuffer(dev, info.width, info.height)
-    r = pt.BasicRenderer(dev, ds, sb)
-    r.set_fused_rounds(0)
+    r = pt.BasicRenderer(dev, ds, sb, rank=a.rank, nranks=a.nranks, streams=a.streams)
+    r.set_fused_rounds(a.fused)
+    r.set_round_batch(a.batch)
     r.RenderFlags = info.render_flags
     r.PathTerminationProbability = info.termination_probability
     r.reset()
@@ -40,11 +46,11 @@ def main():
         r.run(1)
     dev.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.rounds):
-        r.run(1)
+    r.run_rounds(a.rounds)
     dev.synchronize()
     dt = time.perf_counter() - t0
-    print(f"C{a.config} {a.rounds} rounds: {dt / a.rounds * 1e3:.4f} ms per round", flush=True)
+    print(f"C{a.config} rank {a.rank}/{a.nranks} x{a.streams} streams, batch {a.batch}: {a.rounds} rounds, "
+          f"{dt / a.rounds * 1e3:.4f} ms per round, {r.slot_count} slots", flush=True)
     for x in (r, sb, ds, dev):
         x.close()
 
