@@ -640,12 +640,41 @@ PT_DEV bool SampleSurfaceIntegrand(const dscene& S, rng& G, pt3 Nrm, pt3 TX, pt3
 
 // --- path state ----------------------------------------------------------------
 
+
 struct path {
     float Lambda0;
     pt4 Throughput, Probability;
     pt3 Sample;
     uint32_t Active[4];
 };
+
+// The path's four wavelengths from its normalized Lambda0
+// (basic_scatter.glsl:118-122).
+PT_DEV pt4 PathLambda(float L0)
+{
+    return v4(pt_mix(PT_CIE_LAMBDA_MIN, PT_CIE_LAMBDA_MAX, L0),
+              pt_mix(PT_CIE_LAMBDA_MIN, PT_CIE_LAMBDA_MAX, pt_fract(L0 + 0.25f)),
+              pt_mix(PT_CIE_LAMBDA_MIN, PT_CIE_LAMBDA_MAX, pt_fract(L0 + 0.50f)),
+              pt_mix(PT_CIE_LAMBDA_MIN, PT_CIE_LAMBDA_MAX, pt_fract(L0 + 0.75f)));
+}
+
+// An escaped path's contribution (basic_scatter.glsl:165-173): the sky's
+// radiance along V times the throughput, observed (CIE XYZ) and divided by
+// the cluster PDF.
+PT_DEV pt3 EscapeContribution(const dscene& S, pt3 V, pt4 Lambda, pt4 Throughput, float ClusterPDF)
+{
+    pt4 Emission = SampleSkyboxRadiance(S, V, Lambda);
+    pt4 E = Emission * Throughput;
+    // Left-to-right sum over the four wavelengths (the reference's
+    // expression order) as a rolled loop: one observer evaluation's
+    // registers at a time.
+    float Lv[4] = {Lambda.x, Lambda.y, Lambda.z, Lambda.w};
+    float Ev[4] = {E.x, E.y, E.z, E.w};
+    pt3 XYZ = SampleStandardObserver(Lv[0]) * Ev[0];
+#pragma unroll 1
+    for (int I = 1; I < 4; I++) XYZ = XYZ + SampleStandardObserver(Lv[I]) * Ev[I];
+    return XYZ / ClusterPDF;
+}
 
 // Path record (basic.glsl.inc:159-198 StorePathVertex) minus Sample: Scatter
 // adds to Sample only on escape, and the escape zeroes Probability, which
@@ -821,11 +850,7 @@ template <uint32_t MATS>
 PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3& V, uint32_t HitShape,
                     uint32_t HitMaterial, float HitTime, uint32_t PN, uint32_t PT, pt2 UV)
 {
-    float L0 = Path.Lambda0;
-    pt4 Lambda = v4(pt_mix(PT_CIE_LAMBDA_MIN, PT_CIE_LAMBDA_MAX, L0),
-                    pt_mix(PT_CIE_LAMBDA_MIN, PT_CIE_LAMBDA_MAX, pt_fract(L0 + 0.25f)),
-                    pt_mix(PT_CIE_LAMBDA_MIN, PT_CIE_LAMBDA_MAX, pt_fract(L0 + 0.50f)),
-                    pt_mix(PT_CIE_LAMBDA_MIN, PT_CIE_LAMBDA_MAX, pt_fract(L0 + 0.75f)));
+    pt4 Lambda = PathLambda(Path.Lambda0);
 
     uint32_t Active = SHAPE_INDEX_NONE;
     for (int I = 0; I < 4; I++) Active = pt_umin(Active, Path.Active[I]);
@@ -854,18 +879,8 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
             V = normalize(X * Sc.x + Y * Sc.y + Z * Sc.z);
         } else {
             ShadeMark(SM_ESCAPE);
-            pt4 Emission = SampleSkyboxRadiance(S, V, Lambda);
             float ClusterPDF = Path.Probability.x + Path.Probability.y + Path.Probability.z + Path.Probability.w;
-            pt4 E = Emission * Path.Throughput;
-            // Left-to-right sum over the four wavelengths (the reference's
-            // expression order) as a rolled loop: one observer evaluation's
-            // registers at a time.
-            float Lv[4] = {Lambda.x, Lambda.y, Lambda.z, Lambda.w};
-            float Ev[4] = {E.x, E.y, E.z, E.w};
-            pt3 XYZ = SampleStandardObserver(Lv[0]) * Ev[0];
-#pragma unroll 1
-            for (int I = 1; I < 4; I++) XYZ = XYZ + SampleStandardObserver(Lv[I]) * Ev[I];
-            Path.Sample = Path.Sample + XYZ / ClusterPDF;
+            Path.Sample = Path.Sample + EscapeContribution(S, V, Lambda, Path.Throughput, ClusterPDF);
             Path.Probability = v4s(0.0f);
         }
         return max4(Path.Probability) > PT_EPSILON;
@@ -1345,12 +1360,10 @@ PT_DEV void CompletePath(const dscene& S, const dslots& L, const dframe& F, cons
     GenerateNewPath(S, L, F, Pm, G, s, x, y, O, V, act_none);
 }
 
-#ifndef PT_SHADE_COMPACT
-#define PT_SHADE_COMPACT 0
-#endif
-
 // One tile of shade (basic_scatter.glsl:main for the tile's 256 slots).
-template <uint32_t MATS>
+// COMPACT: completion queue (below), for scenes whose paths also end at
+// surfaces (ShadeCompact, runtime.hip).
+template <uint32_t MATS, bool COMPACT = false>
 PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const dparams& Pm, uint32_t tile)
 {
     // One block per tile, no early exit (TileOrder).  ShadeOrder: thread u
@@ -1375,11 +1388,9 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
     bool valid = SlotPixel(F, s, x, y, stream);
     pt3 O = v3s(0), V = v3s(0);
     bool completed = false;
-#if PT_SHADE_COMPACT
-    uint32_t cstate = 0;
+    uint32_t cstate = 0;       // COMPACT: a completed path's RNG state, Sample, empty active stack
     pt3 csample = v3s(0.0f);
     bool cactnone = false;
-#endif
     if (valid) {
         ShadeMark(SM_ENTRY);
         rng G;
@@ -1445,25 +1456,29 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
         } else {
             ShadeMark(SM_COMPLETED);
             completed = true;
-#if PT_SHADE_COMPACT
-            cstate = G.State;
-            csample = P.Sample;
-            cactnone = (act.x & act.y) == 0xFFFFFFFFu;
-#else
-            CompletePath(S, L, F, Pm, G, s, x, y, stream, P.Sample, (act.x & act.y) == 0xFFFFFFFFu, O, V);
-#endif
+            if constexpr (COMPACT) {
+                cstate = G.State;
+                csample = P.Sample;
+                cactnone = (act.x & act.y) == 0xFFFFFFFFu;
+            } else {
+                CompletePath(S, L, F, Pm, G, s, x, y, stream, P.Sample, (act.x & act.y) == 0xFFFFFFFFu, O, V);
+            }
         }
     }
     // Completed paths per wave (ptGetStats): one counter word per 64 slots,
     // updated by the wave's first lane (no atomics: a wave owns its word).
     uint64_t cm = __ballot(completed);
     if ((threadIdx.x & 63u) == 0) L.done[(base | threadIdx.x) >> 6] += (uint32_t)__popcll(cm);
-#if PT_SHADE_COMPACT
-    // Completion queue: the tile's completed paths (scattered over its waves
-    // by the hit / miss / roulette outcomes) are accumulated and restarted by
-    // the first threads of the block, so the camera-ray generation runs in
-    // full waves; the new rays come back through LDS to their slots' threads.
-    {
+    if constexpr (COMPACT) {
+        // Completion queue.  Paths that end at a surface (a sky sample below
+        // the horizon, roulette, a failed BSDF sample) are scattered over the
+        // tile's hit waves, so the completion work -- accumulate, then a new
+        // camera path (GenerateNewPath) -- ran in nearly every wave at a
+        // third of its lanes (C2: 99 % of waves, 25 lanes).  Here the
+        // completed slots are queued in LDS in position order, the first
+        // threads of the block complete them in full waves, and the new rays
+        // come back through LDS to their slots' threads for TileOrder.
+        // The same operations on the same values: bit-identical.
         __shared__ uint32_t cq_slot[256], cq_rng[256], cq_count[4];
         __shared__ float cq_f[6][256];
         const uint32_t w = threadIdx.x >> 6;
@@ -1483,18 +1498,19 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
             cq_f[0][qi] = csample.x; cq_f[1][qi] = csample.y; cq_f[2][qi] = csample.z;
         }
         __syncthreads();
-        if (threadIdx.x < total) {
-            const uint32_t e = cq_slot[threadIdx.x];
+        const uint32_t t = threadIdx.x;
+        if (t < total) {
+            const uint32_t e = cq_slot[t];
             const uint32_t s2 = base | (e & 255u);
             uint32_t x2, y2, stream2;
             (void)SlotPixel(F, s2, x2, y2, stream2);
             rng G2;
-            G2.State = cq_rng[threadIdx.x];
+            G2.State = cq_rng[t];
             pt3 O2, V2;
-            CompletePath(S, L, F, Pm, G2, s2, x2, y2, stream2,
-                         v3(cq_f[0][threadIdx.x], cq_f[1][threadIdx.x], cq_f[2][threadIdx.x]), (e & 256u) != 0, O2, V2);
-            cq_f[0][threadIdx.x] = O2.x; cq_f[1][threadIdx.x] = O2.y; cq_f[2][threadIdx.x] = O2.z;
-            cq_f[3][threadIdx.x] = V2.x; cq_f[4][threadIdx.x] = V2.y; cq_f[5][threadIdx.x] = V2.z;
+            CompletePath(S, L, F, Pm, G2, s2, x2, y2, stream2, v3(cq_f[0][t], cq_f[1][t], cq_f[2][t]), (e & 256u) != 0,
+                         O2, V2);
+            cq_f[0][t] = O2.x; cq_f[1][t] = O2.y; cq_f[2][t] = O2.z;   // each thread rewrites only its own entry
+            cq_f[3][t] = V2.x; cq_f[4][t] = V2.y; cq_f[5][t] = V2.z;
         }
         __syncthreads();
         if (completed) {
@@ -1502,18 +1518,17 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
             V = v3(cq_f[3][qi], cq_f[4][qi], cq_f[5][qi]);
         }
     }
-#endif
     TileOrderStoreRay(L, s, valid, O, V, p16 >> 8);
 }
 
-template <uint32_t MATS>
+template <uint32_t MATS, bool COMPACT>
 __global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void shade_kernel(dscene S, dslots L, dframe F,
                                                                                     dparams Pm)
 {
     // Tiles in extend's longest-first order too: tiles with long traversals
     // also shade more hits (C5 shade -3 %).
     ShadeStatsBegin();
-    ShadeTile<MATS>(S, L, F, Pm, L.order ? L.order[blockIdx.x] : blockIdx.x);
+    ShadeTile<MATS, COMPACT>(S, L, F, Pm, L.order ? L.order[blockIdx.x] : blockIdx.x);
     ShadeStatsEnd();
 }
 
@@ -1846,26 +1861,35 @@ uint32_t pt_shade_mats(uint32_t scene_mats)
     return PT_MATS_ALL | PT_MATS_OPENPBR;
 }
 
-hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
-                           uint32_t scene_mats, hipStream_t st)
+template <bool COMPACT>
+static void LaunchShade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
+                        uint32_t scene_mats, hipStream_t st)
 {
-    if (L.n == 0 || L.tile_count == 0) return hipSuccess;
     switch (pt_shade_mats(scene_mats)) {
     case PT_MATS_DIFFUSE:
-        hipLaunchKernelGGL(ptd::shade_kernel<PT_MATS_DIFFUSE>, dim3(L.tile_count), dim3(256), 0, st, S, L, F, P);
+        hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_DIFFUSE, COMPACT>), dim3(L.tile_count), dim3(256), 0, st, S, L, F,
+                           P);
         break;
     case PT_MATS_DIFFUSE | PT_MATS_METAL:
-        hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_DIFFUSE | PT_MATS_METAL>), dim3(L.tile_count), dim3(256), 0, st,
-                           S, L, F, P);
+        hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_DIFFUSE | PT_MATS_METAL, COMPACT>), dim3(L.tile_count), dim3(256),
+                           0, st, S, L, F, P);
         break;
     case PT_MATS_ALL:
-        hipLaunchKernelGGL(ptd::shade_kernel<PT_MATS_ALL>, dim3(L.tile_count), dim3(256), 0, st, S, L, F, P);
+        hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_ALL, COMPACT>), dim3(L.tile_count), dim3(256), 0, st, S, L, F, P);
         break;
     default:
-        hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_ALL | PT_MATS_OPENPBR>), dim3(L.tile_count), dim3(256), 0, st,
-                           S, L, F, P);
+        hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_ALL | PT_MATS_OPENPBR, COMPACT>), dim3(L.tile_count), dim3(256),
+                           0, st, S, L, F, P);
         break;
     }
+}
+
+hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
+                           uint32_t scene_mats, bool compact, hipStream_t st)
+{
+    if (L.n == 0 || L.tile_count == 0) return hipSuccess;
+    if (compact) LaunchShade<true>(S, L, F, P, scene_mats, st);
+    else LaunchShade<false>(S, L, F, P, scene_mats, st);
     return hipGetLastError();
 }
 

@@ -89,8 +89,10 @@ hipError_t pt_launch_preview(const ptd::dscene& S, const pt_preview_parameters* 
 uint32_t pt_preview_stack_cap();
 hipError_t pt_launch_resolve(const float4* accum, uint32_t n, float brightness, uint32_t mode, float white, float4* out,
                              uint32_t* out8, hipStream_t st);
+// compact: the completion-queue instantiation (ShadeTile), for scenes whose
+// paths also end at surfaces.
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
-                           uint32_t scene_mats, hipStream_t st);
+                           uint32_t scene_mats, bool compact, hipStream_t st);
 hipError_t pt_launch_vertex_decode(const uint2* v, uint32_t n, float4* attr, float* vv, hipStream_t st);
 hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st);
 // Fused round (extend + shade per tile in one launch, round_kernel): the

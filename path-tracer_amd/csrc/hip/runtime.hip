@@ -993,6 +993,20 @@ static uint32_t ShadeMats(const pt_basic_renderer* r)
     return m | PT_MATS_SCATTER;
 }
 
+// Completion queue of the shade kernel (kernels.hip ShadeTile): worth its
+// barriers when paths also end at surfaces -- sky light sampling (a sample
+// below the horizon ends the path), roulette, or metal / translucent /
+// OpenPBR BSDFs (failed samples) -- so that completions are scattered over
+// the hit waves.  Measured (profiles/r04_ab3): C2 shade -3.7 %, C5 -3.0 %;
+// C3 (diffuse, no light sampling, no roulette: every completion is an escape,
+// already grouped by ShadeOrder) +3 % with it, so it stays off there.
+static bool ShadeCompact(const pt_basic_renderer* r)
+{
+    const uint32_t m = ShadeMats(r);
+    return (m & (PT_MATS_METAL | PT_MATS_TRANSLUCENT | PT_MATS_OPENPBR)) != 0 ||
+           r->scene->d.g.SkyboxSamplingProbability > 0.0f || r->params.PathTerminationProbability > 0.0f;
+}
+
 static bool RoundFused(const pt_basic_renderer* r, const ptd::dslots& g)
 {
     const int mode = r->fused;
@@ -1029,7 +1043,7 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
             PT_HIP(pt_launch_extend(r->scene->d, L, F, L.spill, d->stream));
             if (int e = EndTimed(d, ep)) return e;
             if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled)) return e;
-            PT_HIP(pt_launch_shade(r->scene->d, L, F, P, ShadeMats(r), d->stream));
+            PT_HIP(pt_launch_shade(r->scene->d, L, F, P, ShadeMats(r), ShadeCompact(r), d->stream));
             if (int e = EndTimed(d, ep)) return e;
         }
         if (sort) PT_HIP(pt_launch_tile_order(L, d->stream));

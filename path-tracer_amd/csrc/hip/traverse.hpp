@@ -596,10 +596,11 @@ PT_DEV float4 CompactHit(const lane_state& Ln, bool vidx21)
 // Hit attribute reconstruction (scene.glsl.inc:535-608).  Mesh faces: the
 // vertex indices come packed in the hit record (vidx21) or from the face.
 // uv_if_textured: the caller reads the texture coordinates only through the
-// hit material's textures (shade), so hits on shapes whose material samples
-// none (the device shape record's PT_SHAPE_FLAG_UV, loaded with its type)
-// leave them 0 instead of computing them (a sphere's atan2, a mesh's three
-// vertex V loads).
+// hit material's textures (shade), so a sphere hit on a shape whose material
+// samples none (the device shape record's PT_SHAPE_FLAG_UV, loaded with its
+// type) leaves them 0 instead of computing them (an atan2: C2 shade -1.2 %,
+// C5 -1 %).  Other shapes compute them anyway: skipping a mesh's three
+// vertex V loads behind the flag measured C3 shade +1.7 %.
 PT_DEV void HitAttributesV(const dscene& S, uint32_t ShapeIndex, bool packed, uint32_t Z, uint32_t Wd, pt3 C,
                            uint32_t& Material, pt3& Normal, pt3& TangentX, pt2& UV, bool uv_if_textured = false);
 
@@ -630,11 +631,7 @@ PT_DEV void HitAttributesV(const dscene& S, uint32_t ShapeIndex, bool packed, ui
     UV = v2(0.0f, 0.0f);
     const pt_packed_shape* Shape = &S.shapes[ShapeIndex];
     Material = Shape->MaterialIndex;
-#if PT_EXP_UV_ALWAYS
-    const bool uv = true;
-#else
     const bool uv = !uv_if_textured || (Shape->Pad0 & PT_SHAPE_FLAG_UV);
-#endif
     int32_t Type = Shape->Type;
     const float* To = Shape->Transform.To;
     const float* From = Shape->Transform.From;
@@ -655,16 +652,14 @@ PT_DEV void HitAttributesV(const dscene& S, uint32_t ShapeIndex, bool packed, ui
         pt3 N = SafeNormalize(xyz(A0) * C.x + xyz(A1) * C.y + xyz(A2) * C.z);
         Normal = TransformNormal(N, From);
         TangentX = ComputeTangentVector(Normal);
-        if (uv) {
-            pt2 UV0 = v2(A0.w, S.vertex_v[i0]);
-            pt2 UV1 = v2(A1.w, S.vertex_v[i1]);
-            pt2 UV2 = v2(A2.w, S.vertex_v[i2]);
-            UV = UV0 * C.x + UV1 * C.y + UV2 * C.z;
-        }
+        pt2 UV0 = v2(A0.w, S.vertex_v[i0]);
+        pt2 UV1 = v2(A1.w, S.vertex_v[i1]);
+        pt2 UV2 = v2(A2.w, S.vertex_v[i2]);
+        UV = UV0 * C.x + UV1 * C.y + UV2 * C.z;
     } else if (Type == PT_SHAPE_TYPE_PLANE) {
         Normal = TransformNormal(v3(0, 0, 1), From);
         TangentX = TransformDirection(v3(1, 0, 0), To);
-        if (uv) UV = v2(pt_fract(C.x), pt_fract(C.y));
+        UV = v2(pt_fract(C.x), pt_fract(C.y));
     } else if (Type == PT_SHAPE_TYPE_SPHERE) {
         pt3 P = C;
         Normal = TransformNormal(P, From);

@@ -1,10 +1,13 @@
 """What the reciprocal slab-test convention changes against IEEE division.
 
 The device and the oracle evaluate the slab test's (Min - O) / V
-(common.glsl.inc:157-158) as RN((Min - O) * RN(1/V)).  SURVEY.md
-§7/§8(c) wrote the convention down as correctly rounded IEEE division.  This
-script runs the CPU oracle in both conventions (oracle_set_slab_division) on
-the same inputs and reports, per scene:
+(common.glsl.inc:157-158) as correctly rounded IEEE division, the convention
+SURVEY.md §7/§8(c) wrote down (the device reaches it through an
+FMA-corrected reciprocal).  Round 2 had used the reciprocal form
+RN((Min - O) * RN(1/V)); it is kept in the oracle only for this measurement
+(oracle_set_slab_division(0)), which showed it is not a conforming
+restatement.  This script runs the CPU oracle in both conventions on the same
+inputs and reports, per scene:
 
 * rays:  hit-record differences over 20 000 random rays (the parity tests'
   generator) and over the path rays of a rendered frame (each slot's next ray
