@@ -71,13 +71,14 @@ def load_package():
     return mod
 
 
-def profile_for(config):
-    """The committed PMC summary of this config's bench (profiles/traffic.json,
-    keyed by config; tools/update_traffic.py), or None."""
+def profile_for(key):
+    """The committed PMC summary of this workload (profiles/traffic.json,
+    keyed by config, or "CONFIG:bandsNxK" for rank 0 of N band partitions
+    with K path streams; tools/update_traffic.py), or None."""
     p = ROOT / "profiles" / "traffic.json"
     if not p.exists():
         return None
-    return json.loads(p.read_text()).get("configs", {}).get(str(config))
+    return json.loads(p.read_text()).get("configs", {}).get(str(key))
 
 
 def cpu_model():
@@ -411,14 +412,17 @@ def main():
                              "launches": n_k, "rounds": rounds_k}
     # traversal-level cache rate below: extend's time per round, or the fused kernels'
     avg_ext = next(kernels[k]["avg_ms"] for k in ("extend", "round", "rounds") if k in kernels)
-    dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
+    # The dominant kernel: the most device time over the timed rounds (C1's
+    # frames are mostly round batches, with two single fused rounds each).
+    dom = max(kernels, key=lambda k: kernels[k]["avg_ms"] * kernels[k]["rounds"])
     achieved = kernels[dom]["gbps"]
-    prof = profile_for(args.config) or {}
+    # The committed PMC profile of this workload: the whole frame's launches
+    # (N = 1 and sample shards), or rank 0's band partition with its path
+    # streams (a launch over other slots than the whole frame's).
+    pkey = str(args.config) if part_n == 1 else f"{args.config}:bands{part_n}x{streams}"
+    prof = profile_for(pkey) or {}
     kprof = prof.get("kernels", {}).get(dom, {})
-    # The committed PMC profile holds the N=1 whole-frame launches; a band
-    # partition's launches cover 1/N of the slots, so its per-launch bytes do
-    # not apply.
-    traffic = kprof.get("hbm_bytes") if part_n == 1 else None
+    traffic = kprof.get("hbm_bytes")
     xname = "RCCL" if exchange == "rccl" else "gloo (host-memory fallback)"
     metric = ("Mrays/s + Msamples/s, Viking Room 1920x1080 1024spp, 1/2/4/8 GPUs" if args.config == 3 and spp == 1024
               else f"Mrays/s + Msamples/s, C{args.config} {info.width}x{info.height} {spp}spp")
@@ -491,8 +495,9 @@ def main():
         # active lanes per VALU instruction (of 64; divergence).  null when no
         # profile of this config is committed.
         "limiter": ({"kind": "valu_issue", "kernel": dom, **(prof.get("issue", {}).get(dom) or {}),
-                     "per_kernel": {k: prof.get("issue", {}).get(k) for k in ("extend", "shade")},
-                     "source": prof.get("profile")} if prof and part_n == 1 else None),
+                     "per_kernel": {k: prof.get("issue", {}).get(k) for k in ("extend", "shade", "round", "rounds")
+                                    if prof.get("issue", {}).get(k)},
+                     "source": prof.get("profile"), "profile_key": pkey} if prof else None),
     }
     # Node/face bytes the traversal pulls through L1/L2 per ray (BVH + faces
     # are cache-resident): internal node = both child boxes (64 B), face 48 B,

@@ -16,7 +16,7 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-VARIANT = ROOT / "build" / "variants" / "shadestats.so"
+VARIANT = Path(os.environ.get("PT_STATS_LIB", ROOT / "build" / "variants" / "shadestats.so"))
 os.environ["PT_HIP_LIB"] = str(VARIANT)
 sys.path.insert(0, str(ROOT))
 import bench  # noqa: E402  (package loader)
