@@ -1541,192 +1541,6 @@ PT_DEV void ShadeTile(const dscene& S, const dslots& L, const dframe& F, const d
     TileOrderStoreRay(L, s, valid, O, V, p16 >> 8);
 }
 
-// Pooled shade (PT_SHADE_TILES = MT > 1): one block of MT x 256 threads
-// shades MT tiles with ShadeOrder pooled over them.  A tile has 256
-// positions in up to five outcome classes (hit by material type, miss); a
-// class boundary inside a wave makes that wave run both classes' code, and
-// with four or five classes nearly every wave of a tile straddled one (C5:
-// 1.64 classes per wave).  Here the block orders the positions of its tiles
-// class by class (class-major, then tile), so a boundary costs one mixed
-// wave per 4 x MT waves.  The new rays go through LDS to the threads of their
-// own tile for TileOrder.  (A 256-thread block looping over the tiles kept
-// the scene's loop-invariant values live across the inlined body and spilled
-// 37-95 VGPRs: 1.5-2.5x slower; as a called function, slower still.)
-template <uint32_t MT>
-PT_DEV void TileOrderStorePooled(const dslots& L, uint32_t s, uint32_t key, float4 ray, uint32_t hitbyte, bool store)
-{
-    __shared__ uint32_t cnt[MT][64];
-    const uint32_t g = threadIdx.x >> 8, w = (threadIdx.x >> 6) & 3u, lane = threadIdx.x & 63u;
-    uint32_t rank = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 9; k++) {
-        uint64_t m = __ballot(key == k);
-        uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (key == k) rank = below;
-        if (lane == 0) cnt[g][k * 4 + w] = (uint32_t)__popcll(m);
-    }
-    __syncthreads();
-    uint32_t v = lane < 36 ? cnt[g][lane] : 0u;
-    uint32_t incl = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t t = (uint32_t)__shfl_up((int)incl, o, 64);
-        if ((int)lane >= o) incl += t;
-    }
-    uint32_t base = (uint32_t)__shfl((int)(incl - v), (int)(key * 4 + w), 64);
-    uint32_t p = base + rank;
-    uint32_t q = (s & ~255u) | p;
-    if (!store) return;   // a thread of a missing tile (partial last block)
-    L.ray[q] = ray;
-    L.pos[s] = (uint16_t)((p << 8) | hitbyte);
-    L.slotof[q] = (uint8_t)(s & 255u);
-}
-
-// The completion queue over a pooled block (CompletionQueue for MT x 256).
-template <uint32_t MT>
-PT_DEV void CompletionQueuePooled(const dscene& S, const dslots& L, const dframe& F, const dparams& Pm, uint32_t s,
-                                  bool completed, uint64_t cm, uint32_t cstate, pt3 csample, bool cactnone, pt3& O,
-                                  pt3& V)
-{
-    constexpr uint32_t N = MT * 256;
-    __shared__ uint32_t cq_slot[N], cq_rng[N], cq_count[MT * 4];
-    __shared__ float cq_f[6][N];
-    const uint32_t w = threadIdx.x >> 6;
-    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
-    if ((threadIdx.x & 63u) == 0) cq_count[w] = (uint32_t)__popcll(cm);
-    __syncthreads();
-    uint32_t qi = below, total = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < MT * 4; k++) {
-        const uint32_t c = cq_count[k];
-        qi += k < w ? c : 0u;
-        total += c;
-    }
-    if (completed) {
-        cq_slot[qi] = s | (cactnone ? 0x80000000u : 0u);
-        cq_rng[qi] = cstate;
-        cq_f[0][qi] = csample.x; cq_f[1][qi] = csample.y; cq_f[2][qi] = csample.z;
-    }
-    __syncthreads();
-    const uint32_t t = threadIdx.x;
-    if (t < total) {
-        const uint32_t e = cq_slot[t];
-        const uint32_t s2 = e & 0x7FFFFFFFu;
-        uint32_t x2, y2, stream2;
-        (void)SlotPixel(F, s2, x2, y2, stream2);
-        rng G2;
-        G2.State = cq_rng[t];
-        pt3 O2, V2;
-        CompletePath(S, L, F, Pm, G2, s2, x2, y2, stream2, v3(cq_f[0][t], cq_f[1][t], cq_f[2][t]),
-                     (e & 0x80000000u) != 0, O2, V2);
-        cq_f[0][t] = O2.x; cq_f[1][t] = O2.y; cq_f[2][t] = O2.z;
-        cq_f[3][t] = V2.x; cq_f[4][t] = V2.y; cq_f[5][t] = V2.z;
-    }
-    __syncthreads();
-    if (completed) {
-        O = v3(cq_f[0][qi], cq_f[1][qi], cq_f[2][qi]);
-        V = v3(cq_f[3][qi], cq_f[4][qi], cq_f[5][qi]);
-    }
-}
-
-template <uint32_t MATS, bool COMPACT, uint32_t MT>
-PT_DEV void ShadeTiles(const dscene& S, const dslots& L, const dframe& F, const dparams& Pm, uint32_t first_block)
-{
-    constexpr uint32_t NC = PT_OUTCOME_CLASSES;
-    __shared__ uint64_t smask[MT * NC * 4];
-    __shared__ uint32_t scnt[MT * NC * 4];
-    __shared__ uint32_t sstart[MT * NC + 1];
-    __shared__ uint32_t stile[MT];
-    __shared__ float4 sray[MT * 256];      // new ray: origin, packed direction (by tile, slot)
-    __shared__ uint16_t skey[MT * 256];    // TileOrder key (bits 8-11) | hit byte (bits 0-7)
-    const uint32_t nt = min(MT, L.tile_count - first_block);
-    const uint32_t tid = threadIdx.x;
-    if (tid < MT) stile[tid] = tid < nt ? (L.order ? L.order[first_block + tid] : first_block + tid) : 0u;
-    __syncthreads();
-    // Class masks of the tiles (single-material scenes store the miss class
-    // only: hits are its complement), their popcounts, then the pooled start
-    // of each (class, tile) segment.
-    if (tid < MT * NC * 4) {
-        const uint32_t j = tid / (NC * 4), r = tid % (NC * 4), c = r >> 2, w = r & 3u;
-        uint64_t m = 0;
-        if (j < nt) {
-            const uint64_t* om = L.outcome + (size_t)stile[j] * (4 * NC);
-            m = S.mat_classes ? om[r] : c == 0 ? ~om[4 * (NC - 1) + w] : c == NC - 1 ? om[4 * (NC - 1) + w] : 0ull;
-        }
-        smask[tid] = m;
-        scnt[tid] = (uint32_t)__popcll(m);
-    }
-    __syncthreads();
-    if (tid < 64) {
-        // segment t = c * MT + j (class-major); exclusive scan over one wave
-        uint32_t n = 0;
-        if (tid < MT * NC) {
-            const uint32_t c = tid / MT, j = tid % MT;
-            const uint32_t* k = &scnt[j * NC * 4 + c * 4];
-            n = k[0] + k[1] + k[2] + k[3];
-        }
-        uint32_t incl = n;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            uint32_t t = (uint32_t)__shfl_up((int)incl, o, 64);
-            if ((int)tid >= o) incl += t;
-        }
-        if (tid < MT * NC) sstart[tid] = incl - n;
-        if (tid == MT * NC - 1) sstart[MT * NC] = incl;
-    }
-    __syncthreads();
-    // Thread u shades pooled position u (positions of the missing tiles of a
-    // last, partial block are idle threads).
-    const uint32_t u = tid;
-    const bool live = u < nt * 256;
-    uint32_t j = 0, pq = 0;
-    if (live) {
-        // the segment holding u: the last one starting at or before it
-        // (empty segments share their start with the next)
-        uint32_t seg = 0;
-#pragma unroll
-        for (uint32_t b = 32; b >= 1; b >>= 1)
-            if (seg + b < MT * NC && sstart[seg + b] <= u) seg += b;
-        const uint32_t c = seg / MT;
-        j = seg % MT;
-        uint32_t k = u - sstart[seg];
-        const uint32_t* cw = &scnt[j * NC * 4 + c * 4];
-        uint32_t word = 0;
-        if (k >= cw[0]) { k -= cw[0]; word = 1;
-            if (k >= cw[1]) { k -= cw[1]; word = 2;
-                if (k >= cw[2]) { k -= cw[2]; word = 3; } } }
-        pq = word * 64 + SelectBit64(smask[j * NC * 4 + c * 4 + word], k);
-    }
-    const uint32_t base = stile[j] * 256;
-    const uint32_t sl = live ? L.slotof[base | pq] : 0u;
-    const uint32_t s = base | sl;
-    uint32_t x, y, stream;
-    const bool valid = live && SlotPixel(F, s, x, y, stream);
-    pt3 O = v3s(0), V = v3s(0);
-    bool completed = false;
-    uint32_t cstate = 0;
-    pt3 csample = v3s(0.0f);
-    bool cactnone = false;
-    ShadeSlot<MATS, COMPACT>(S, L, F, Pm, s, pq << 8, x, y, stream, valid, O, V, completed, cstate, csample, cactnone);
-    const uint64_t cm = __ballot(completed);
-    if ((tid & 63u) == 0 && (tid >> 8) < nt) L.done[(size_t)stile[tid >> 8] * 4 + ((tid >> 6) & 3u)] += (uint32_t)__popcll(cm);
-    if constexpr (COMPACT) CompletionQueuePooled<MT>(S, L, F, Pm, s, completed, cm, cstate, csample, cactnone, O, V);
-    if (live) {
-        sray[j * 256 + sl] = make_float4(O.x, O.y, O.z, __uint_as_float(PackUnitVector(V)));
-        skey[j * 256 + sl] = (uint16_t)((TileOrderKey(valid, V) << 8) | pq);
-    }
-    __syncthreads();
-    // Thread g * 256 + t stores slot t of tile g (TileOrder per tile).
-    const uint32_t g = tid >> 8, t = tid & 255u;
-    const uint32_t e = skey[tid];
-    TileOrderStorePooled<MT>(L, stile[g] * 256 + t, g < nt ? e >> 8 : 8u, sray[tid], e & 255u, g < nt);
-}
-
-// Tiles per shade block (ShadeTiles; 1 = ShadeTile).
-#ifndef PT_SHADE_TILES
-#define PT_SHADE_TILES 1
-#endif
-
 template <uint32_t MATS, bool COMPACT>
 __global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void shade_kernel(dscene S, dslots L, dframe F,
                                                                                     dparams Pm)
@@ -1738,16 +1552,6 @@ __global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void shade_kernel(dscen
     ShadeStatsEnd();
 }
 
-// Pooled shade blocks of MT tiles (ShadeTiles): MT x 256 threads, so a CU
-// holds 5 / MT blocks' waves per SIMD at most; the VGPR budget is that of
-// floor(5 / MT) * MT waves per SIMD.
-template <uint32_t MATS, bool COMPACT, uint32_t MT>
-__global__ __launch_bounds__(MT * 256) void shade_pooled_kernel(dscene S, dslots L, dframe F, dparams Pm)
-{
-    ShadeStatsBegin();
-    ShadeTiles<MATS, COMPACT, MT>(S, L, F, Pm, blockIdx.x * MT);
-    ShadeStatsEnd();
-}
 
 // One round (extend + shade) of a tile per block, for partitions whose tiles
 // all fit on the GPU at once (a rank's share of a strongly scaled frame):
@@ -2083,29 +1887,6 @@ static void LaunchShade(const ptd::dscene& S, const ptd::dslots& L, const ptd::d
                         uint32_t scene_mats, hipStream_t st)
 {
     const uint32_t blocks = L.tile_count;
-    if constexpr (PT_SHADE_TILES > 1) {
-        constexpr uint32_t MT = PT_SHADE_TILES;
-        const uint32_t pb = (L.tile_count + MT - 1) / MT;
-        switch (pt_shade_mats(scene_mats)) {
-        case PT_MATS_DIFFUSE:
-            hipLaunchKernelGGL((ptd::shade_pooled_kernel<PT_MATS_DIFFUSE, COMPACT, MT>), dim3(pb), dim3(MT * 256), 0, st,
-                               S, L, F, P);
-            break;
-        case PT_MATS_DIFFUSE | PT_MATS_METAL:
-            hipLaunchKernelGGL((ptd::shade_pooled_kernel<PT_MATS_DIFFUSE | PT_MATS_METAL, COMPACT, MT>), dim3(pb),
-                               dim3(MT * 256), 0, st, S, L, F, P);
-            break;
-        case PT_MATS_ALL:
-            hipLaunchKernelGGL((ptd::shade_pooled_kernel<PT_MATS_ALL, COMPACT, MT>), dim3(pb), dim3(MT * 256), 0, st, S,
-                               L, F, P);
-            break;
-        default:
-            hipLaunchKernelGGL((ptd::shade_pooled_kernel<PT_MATS_ALL | PT_MATS_OPENPBR, COMPACT, MT>), dim3(pb),
-                               dim3(MT * 256), 0, st, S, L, F, P);
-            break;
-        }
-        return;
-    }
     switch (pt_shade_mats(scene_mats)) {
     case PT_MATS_DIFFUSE:
         hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_DIFFUSE, COMPACT>), dim3(blocks), dim3(256), 0, st, S, L, F, P);
