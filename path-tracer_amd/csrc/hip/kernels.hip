@@ -577,18 +577,36 @@ PT_DEV bool SampleSurfaceIntegrand(const dscene& S, rng& G, pt3 Nrm, pt3 TX, pt3
     pt3 SMD = v3(S.g.SkyboxMeanDirection[0], S.g.SkyboxMeanDirection[1], S.g.SkyboxMeanDirection[2]);
     pt3 Mu = v3(dot(SMD, TX), dot(SMD, TY), dot(SMD, Nrm));
     bool ok;
-    const bool light = G.R01() < LightProbability;
+    // Without PT_MATS_SKY the probability is +-0, so the draw (still made:
+    // the RNG sequence is the reference's) never selects the light.
+    const float Ul = G.R01();
+    const bool light = (MATS & PT_MATS_SKY) && Ul < LightProbability;
     // A diffuse hit draws In by the light choice -- the sky lobe or the
     // material's cosine sample -- and then evaluates the material with the
     // same arguments either way (MaterialEvaluateBSDF / MaterialSampleBSDF of
     // basic_diffuse.glsl.inc), so the evaluation runs once after the join.
-    if (light) {
-        ShadeMark(SM_LIGHT);
-        In = RandomVonMisesFisher(G, vmf_consts{S.vmf_inv_kappa, S.vmf_exp_m2k, S.vmf_norm}, Mu);
-        if (In.z < 0.0f) { ShadeMark(SM_LIGHT_BELOW); return false; }
-    } else if (diffuse) {
-        ShadeMark(SM_DIFFUSE_COSINE);
-        In = SafeNormalize(RandomDirection(G) + v3(0, 0, 1));
+    //
+    // The sky lobe (RandomVonMisesFisher) and the cosine lobe (RandomDirection
+    // + Z) draw the same two numbers into the same spherical construction and
+    // differ only in its height Z and its frame, so a wave holding both kinds
+    // of lane runs the sqrt, the sine / cosine and the normalization once.
+    if (light || diffuse) {
+        const float Xi = G.R01();
+        float Z;
+        pt3 MuX = v3s(0.0f), MuY = v3s(0.0f);
+        if (light) {
+            ShadeMark(SM_LIGHT);
+            Z = 1 + S.vmf_inv_kappa * pt_log(Xi + (1 - Xi) * S.vmf_exp_m2k);
+            ComputeCoordinateFrame(Mu, MuX, MuY);
+        } else {
+            ShadeMark(SM_DIFFUSE_COSINE);
+            Z = 2 * Xi - 1;
+        }
+        const float R = pt_sqrt(1 - Z * Z);
+        const float Phi = G.R01() * PT_TAU;
+        const pt3 D = v3(R * pt_cos(Phi), R * pt_sin(Phi), Z);
+        In = SafeNormalize(light ? D.x * MuX + D.y * MuY + D.z * Mu : D + v3(0, 0, 1));
+        if (light && In.z < 0.0f) { ShadeMark(SM_LIGHT_BELOW); return false; }
     }
     // Reflectances: the diffuse and metal base spectrum share a material word
     // (BASE_SPECTRUM = 1), the metal's specular spectrum; the translucent's
@@ -1349,7 +1367,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(dscene S, uint32_t n, con
 template <uint32_t MATS>
 constexpr int ShadeMinWaves()
 {
-    return MATS == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MINW
+    return (MATS & ~(uint32_t)PT_MATS_SCENE) == PT_MATS_DIFFUSE ? PT_SHADE_DIFFUSE_MINW
          : (MATS & PT_MATS_OPENPBR) ? PT_SHADE_OPENPBR_MINW : PT_SHADE_OTHER_MINW;
 }
 // A completed path (basic_scatter.glsl:344-359): its Sample accumulated into
@@ -1423,7 +1441,8 @@ PT_DEV void ShadeSlot(const dscene& S, const dslots& L, const dframe& F, const d
 #endif
             float2 c = L.uv[q];
             pt3 N, TX;
-            HitAttributesRecord(S, HitShape, h, c, HitMaterial, N, TX, UV, /*uv_if_textured=*/true);
+            HitAttributesRecord(S, HitShape, h, c, HitMaterial, N, TX, UV, /*uv_if_textured=*/true,
+                                /*prims=*/(MATS & PT_MATS_PRIMS) != 0);
             HitMaterial &= 0xFFFFu;
             HitShape &= 0xFFFFu;
             HitTime = h.x;
@@ -1793,15 +1812,15 @@ static const void* RoundKernel() { return reinterpret_cast<const void*>(&ptd::ro
 
 static const void* RoundKernelFor(uint32_t mats, bool stack16)
 {
+    constexpr uint32_t D = PT_MATS_DIFFUSE, DS = PT_MATS_DIFFUSE | PT_MATS_SCENE,
+                       DM = PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_SCENE, A = PT_MATS_ALL | PT_MATS_SCENE,
+                       AO = PT_MATS_ALL | PT_MATS_OPENPBR | PT_MATS_SCENE;
     switch (pt_shade_mats(mats)) {
-    case PT_MATS_DIFFUSE: return stack16 ? RoundKernel<PT_MATS_DIFFUSE, uint16_t>() : RoundKernel<PT_MATS_DIFFUSE, uint32_t>();
-    case PT_MATS_DIFFUSE | PT_MATS_METAL:
-        return stack16 ? RoundKernel<PT_MATS_DIFFUSE | PT_MATS_METAL, uint16_t>()
-                       : RoundKernel<PT_MATS_DIFFUSE | PT_MATS_METAL, uint32_t>();
-    case PT_MATS_ALL: return stack16 ? RoundKernel<PT_MATS_ALL, uint16_t>() : RoundKernel<PT_MATS_ALL, uint32_t>();
-    default:
-        return stack16 ? RoundKernel<PT_MATS_ALL | PT_MATS_OPENPBR, uint16_t>()
-                       : RoundKernel<PT_MATS_ALL | PT_MATS_OPENPBR, uint32_t>();
+    case D: return stack16 ? RoundKernel<D, uint16_t>() : RoundKernel<D, uint32_t>();
+    case DS: return stack16 ? RoundKernel<DS, uint16_t>() : RoundKernel<DS, uint32_t>();
+    case DM: return stack16 ? RoundKernel<DM, uint16_t>() : RoundKernel<DM, uint32_t>();
+    case A: return stack16 ? RoundKernel<A, uint16_t>() : RoundKernel<A, uint32_t>();
+    default: return stack16 ? RoundKernel<AO, uint16_t>() : RoundKernel<AO, uint32_t>();
     }
 }
 
@@ -1843,15 +1862,15 @@ static const void* RoundsKernel() { return reinterpret_cast<const void*>(&ptd::r
 
 static const void* RoundsKernelFor(uint32_t mats, bool stack16)
 {
+    constexpr uint32_t D = PT_MATS_DIFFUSE, DS = PT_MATS_DIFFUSE | PT_MATS_SCENE,
+                       DM = PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_SCENE, A = PT_MATS_ALL | PT_MATS_SCENE,
+                       AO = PT_MATS_ALL | PT_MATS_OPENPBR | PT_MATS_SCENE;
     switch (pt_shade_mats(mats)) {
-    case PT_MATS_DIFFUSE: return stack16 ? RoundsKernel<PT_MATS_DIFFUSE, uint16_t>() : RoundsKernel<PT_MATS_DIFFUSE, uint32_t>();
-    case PT_MATS_DIFFUSE | PT_MATS_METAL:
-        return stack16 ? RoundsKernel<PT_MATS_DIFFUSE | PT_MATS_METAL, uint16_t>()
-                       : RoundsKernel<PT_MATS_DIFFUSE | PT_MATS_METAL, uint32_t>();
-    case PT_MATS_ALL: return stack16 ? RoundsKernel<PT_MATS_ALL, uint16_t>() : RoundsKernel<PT_MATS_ALL, uint32_t>();
-    default:
-        return stack16 ? RoundsKernel<PT_MATS_ALL | PT_MATS_OPENPBR, uint16_t>()
-                       : RoundsKernel<PT_MATS_ALL | PT_MATS_OPENPBR, uint32_t>();
+    case D: return stack16 ? RoundsKernel<D, uint16_t>() : RoundsKernel<D, uint32_t>();
+    case DS: return stack16 ? RoundsKernel<DS, uint16_t>() : RoundsKernel<DS, uint32_t>();
+    case DM: return stack16 ? RoundsKernel<DM, uint16_t>() : RoundsKernel<DM, uint32_t>();
+    case A: return stack16 ? RoundsKernel<A, uint16_t>() : RoundsKernel<A, uint32_t>();
+    default: return stack16 ? RoundsKernel<AO, uint16_t>() : RoundsKernel<AO, uint32_t>();
     }
 }
 
@@ -1876,10 +1895,15 @@ hipError_t pt_launch_rounds(const ptd::dscene& S, const ptd::dslots& L, const pt
 // scene's mask is launched.
 uint32_t pt_shade_mats(uint32_t scene_mats)
 {
+    // Diffuse meshes without sky light sampling (the Viking Room, C3): the
+    // lean instantiation, which has no sky lobe and no analytic shapes.
     if ((scene_mats & ~(uint32_t)PT_MATS_DIFFUSE) == 0) return PT_MATS_DIFFUSE;
-    if ((scene_mats & ~(uint32_t)(PT_MATS_DIFFUSE | PT_MATS_METAL)) == 0) return PT_MATS_DIFFUSE | PT_MATS_METAL;
-    if (!(scene_mats & PT_MATS_OPENPBR)) return PT_MATS_ALL;
-    return PT_MATS_ALL | PT_MATS_OPENPBR;
+    scene_mats |= PT_MATS_SCENE;
+    if ((scene_mats & ~(uint32_t)(PT_MATS_DIFFUSE | PT_MATS_SCENE)) == 0) return PT_MATS_DIFFUSE | PT_MATS_SCENE;
+    if ((scene_mats & ~(uint32_t)(PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_SCENE)) == 0)
+        return PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_SCENE;
+    if (!(scene_mats & PT_MATS_OPENPBR)) return PT_MATS_ALL | PT_MATS_SCENE;
+    return PT_MATS_ALL | PT_MATS_OPENPBR | PT_MATS_SCENE;
 }
 
 template <bool COMPACT>
@@ -1891,16 +1915,21 @@ static void LaunchShade(const ptd::dscene& S, const ptd::dslots& L, const ptd::d
     case PT_MATS_DIFFUSE:
         hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_DIFFUSE, COMPACT>), dim3(blocks), dim3(256), 0, st, S, L, F, P);
         break;
-    case PT_MATS_DIFFUSE | PT_MATS_METAL:
-        hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_DIFFUSE | PT_MATS_METAL, COMPACT>), dim3(blocks), dim3(256), 0,
-                           st, S, L, F, P);
+    case PT_MATS_DIFFUSE | PT_MATS_SCENE:
+        hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_DIFFUSE | PT_MATS_SCENE, COMPACT>), dim3(blocks), dim3(256), 0, st,
+                           S, L, F, P);
         break;
-    case PT_MATS_ALL:
-        hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_ALL, COMPACT>), dim3(blocks), dim3(256), 0, st, S, L, F, P);
+    case PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_SCENE:
+        hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_SCENE, COMPACT>), dim3(blocks),
+                           dim3(256), 0, st, S, L, F, P);
+        break;
+    case PT_MATS_ALL | PT_MATS_SCENE:
+        hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_ALL | PT_MATS_SCENE, COMPACT>), dim3(blocks), dim3(256), 0, st, S,
+                           L, F, P);
         break;
     default:
-        hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_ALL | PT_MATS_OPENPBR, COMPACT>), dim3(blocks), dim3(256), 0, st,
-                           S, L, F, P);
+        hipLaunchKernelGGL((ptd::shade_kernel<PT_MATS_ALL | PT_MATS_OPENPBR | PT_MATS_SCENE, COMPACT>), dim3(blocks),
+                           dim3(256), 0, st, S, L, F, P);
         break;
     }
 }

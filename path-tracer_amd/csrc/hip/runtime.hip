@@ -117,7 +117,7 @@ struct pt_scene {
     bool atlas_tiled = false;    // atlas in AtlasIndex 4x2-texel blocks
     uint32_t camera_count = 0;
     uint32_t stack_needed = 0;   // max traversal stack entries (TLAS + BLAS)
-    uint32_t mats = PT_MATS_ALL; // material types referenced by shapes (shade specialisation)
+    uint32_t mats = PT_MATS_ALL | PT_MATS_SCENE; // SceneMaterialMask (shade specialisation)
     uint32_t stack_format = PT_STACK_FORMAT_AUTO;   // ptSetSceneStackFormat (applied at the next update)
     uint32_t hit_record = PT_HIT_RECORD_AUTO;       // ptSetSceneHitRecordForm (applied at the next update)
     bool valid = false;
@@ -620,8 +620,10 @@ static bool MaterialReadsUV(const pt_scene_packs* p, uint32_t m)
     }
 }
 
-// Material types reachable by a hit (every shape's material) plus whether any
-// medium can scatter: selects the shade kernel instantiation (kernels.hip).
+// Material types reachable by a hit (every shape's material), whether any
+// medium can scatter, whether any shape is not a mesh instance and whether sky
+// light sampling is on: selects the shade kernel instantiation (kernels.hip
+// pt_shade_mats).
 static uint32_t SceneMaterialMask(const pt_scene_packs* p)
 {
     uint32_t m = 0;
@@ -633,6 +635,9 @@ static uint32_t SceneMaterialMask(const pt_scene_packs* p)
         else if (type == PT_MATERIAL_TYPE_OPENPBR) m |= PT_MATS_OPENPBR;
     }
     if ((m & PT_MATS_TRANSLUCENT) || p->globals->SceneScatterRate > 0.0f) m |= PT_MATS_SCATTER;
+    for (uint32_t i = 0; i < p->shape_count; i++)
+        if (p->shapes[i].Type != PT_SHAPE_TYPE_MESH_INSTANCE) m |= PT_MATS_PRIMS;
+    if (!(p->globals->SkyboxSamplingProbability == 0.0f)) m |= PT_MATS_SKY;
     return m;
 }
 

@@ -600,9 +600,12 @@ PT_DEV float4 CompactHit(const lane_state& Ln, bool vidx21)
 // samples none (the device shape record's PT_SHAPE_FLAG_UV, loaded with its
 // type) leaves them 0 instead of computing them (an atan2: C2 shade -1.2 %,
 // C5 -1 %).  Other shapes compute them anyway: skipping a mesh's three
-// vertex V loads behind the flag measured C3 shade +1.7 %.
+// vertex V loads behind the flag measured C3 shade +1.7 %.  prims false
+// (the shade instantiation of a mesh-only scene) compiles out the other
+// shape types.
 PT_DEV void HitAttributesV(const dscene& S, uint32_t ShapeIndex, bool packed, uint32_t Z, uint32_t Wd, pt3 C,
-                           uint32_t& Material, pt3& Normal, pt3& TangentX, pt2& UV, bool uv_if_textured = false);
+                           uint32_t& Material, pt3& Normal, pt3& TangentX, pt2& UV, bool uv_if_textured = false,
+                           bool prims = true);
 
 PT_DEV void HitAttributes(const dscene& S, uint32_t ShapeIndex, uint32_t Prim, pt3 C, uint32_t& Material, pt3& Normal,
                           pt3& TangentX, pt2& UV)
@@ -612,21 +615,21 @@ PT_DEV void HitAttributes(const dscene& S, uint32_t ShapeIndex, uint32_t Prim, p
 
 // From a compact hit record (h = {Time, Shape, z, w}, c = {C.y, C.z}).
 PT_DEV void HitAttributesRecord(const dscene& S, uint32_t ShapeIndex, float4 h, float2 c, uint32_t& Material,
-                                pt3& Normal, pt3& TangentX, pt2& UV, bool uv_if_textured = false)
+                                pt3& Normal, pt3& TangentX, pt2& UV, bool uv_if_textured = false, bool prims = true)
 {
-    const bool mesh = S.shapes[ShapeIndex].Type == PT_SHAPE_TYPE_MESH_INSTANCE;
+    const bool mesh = !prims || S.shapes[ShapeIndex].Type == PT_SHAPE_TYPE_MESH_INSTANCE;
     if (S.vidx21) {
         pt3 C = mesh ? v3(1 - c.x - c.y, c.x, c.y) : v3(h.z, c.x, c.y);
         HitAttributesV(S, ShapeIndex, true, __float_as_uint(h.z), __float_as_uint(h.w), C, Material, Normal, TangentX, UV,
-                       uv_if_textured);
+                       uv_if_textured, prims);
     } else {
         HitAttributesV(S, ShapeIndex, false, __float_as_uint(h.z), 0u, v3(h.w, c.x, c.y), Material, Normal, TangentX, UV,
-                       uv_if_textured);
+                       uv_if_textured, prims);
     }
 }
 
 PT_DEV void HitAttributesV(const dscene& S, uint32_t ShapeIndex, bool packed, uint32_t Z, uint32_t Wd, pt3 C,
-                           uint32_t& Material, pt3& Normal, pt3& TangentX, pt2& UV, bool uv_if_textured)
+                           uint32_t& Material, pt3& Normal, pt3& TangentX, pt2& UV, bool uv_if_textured, bool prims)
 {
     UV = v2(0.0f, 0.0f);
     const pt_packed_shape* Shape = &S.shapes[ShapeIndex];
@@ -635,7 +638,13 @@ PT_DEV void HitAttributesV(const dscene& S, uint32_t ShapeIndex, bool packed, ui
     int32_t Type = Shape->Type;
     const float* To = Shape->Transform.To;
     const float* From = Shape->Transform.From;
-    if (Type == PT_SHAPE_TYPE_MESH_INSTANCE) {
+    // Each shape type yields its object-space normal and tangent; the
+    // transforms to world space run once after the join (a wave with
+    // spheres, cubes and planes runs them once, not per type).
+    // prims false: the scene has mesh instances only (PT_MATS_PRIMS clear).
+    const bool mesh = !prims || Type == PT_SHAPE_TYPE_MESH_INSTANCE;
+    pt3 N, T = v3s(0.0f);
+    if (mesh) {
         uint32_t i0, i1, i2;
         if (packed) {
             UnpackVertexIndices(Z, Wd, i0, i1, i2);
@@ -649,21 +658,19 @@ PT_DEV void HitAttributesV(const dscene& S, uint32_t ShapeIndex, bool packed, ui
         float4 A0 = S.vertex_attr[i0];
         float4 A1 = S.vertex_attr[i1];
         float4 A2 = S.vertex_attr[i2];
-        pt3 N = SafeNormalize(xyz(A0) * C.x + xyz(A1) * C.y + xyz(A2) * C.z);
-        Normal = TransformNormal(N, From);
-        TangentX = ComputeTangentVector(Normal);
+        N = SafeNormalize(xyz(A0) * C.x + xyz(A1) * C.y + xyz(A2) * C.z);
         pt2 UV0 = v2(A0.w, S.vertex_v[i0]);
         pt2 UV1 = v2(A1.w, S.vertex_v[i1]);
         pt2 UV2 = v2(A2.w, S.vertex_v[i2]);
         UV = UV0 * C.x + UV1 * C.y + UV2 * C.z;
     } else if (Type == PT_SHAPE_TYPE_PLANE) {
-        Normal = TransformNormal(v3(0, 0, 1), From);
-        TangentX = TransformDirection(v3(1, 0, 0), To);
+        N = v3(0, 0, 1);
+        T = v3(1, 0, 0);
         UV = v2(pt_fract(C.x), pt_fract(C.y));
     } else if (Type == PT_SHAPE_TYPE_SPHERE) {
         pt3 P = C;
-        Normal = TransformNormal(P, From);
-        TangentX = TransformDirection(cross(P, v3(-P.y, P.x, 0)), To);
+        N = P;
+        T = cross(P, v3(-P.y, P.x, 0));
         if (uv) {
             float U = (pt_atan2(P.y, P.x) + PT_PI) / PT_TAU;
             float W = (P.z + 1.0f) / 2.0f;
@@ -672,7 +679,6 @@ PT_DEV void HitAttributesV(const dscene& S, uint32_t ShapeIndex, bool packed, ui
     } else {
         pt3 P = C;
         pt3 Q = vabs(P);
-        pt3 N, T;
         if (Q.x >= Q.y && Q.x >= Q.z) {
             float Sg = pt_sign(P.x);
             N = v3(Sg, 0, 0); T = v3(0, Sg, 0);
@@ -686,9 +692,9 @@ PT_DEV void HitAttributesV(const dscene& S, uint32_t ShapeIndex, bool packed, ui
             N = v3(0, 0, Sg); T = v3(Sg, 0, 0);
             UV = 0.5f * v2(1.0f + P.x, 1.0f + P.y);
         }
-        Normal = TransformNormal(N, From);
-        TangentX = TransformDirection(T, To);
     }
+    Normal = TransformNormal(N, From);
+    TangentX = mesh ? ComputeTangentVector(Normal) : TransformDirection(T, To);
 }
 
 }  // namespace ptd
