@@ -611,7 +611,9 @@ PT_DEV bool SampleSurfaceIntegrand(const dscene& S, rng& G, pt3 Nrm, pt3 TX, pt3
     // Reflectances: the diffuse and metal base spectrum share a material word
     // (BASE_SPECTRUM = 1), the metal's specular spectrum; the translucent's
     // Cauchy IOR relative to the exterior on Out's side.
-    if (diffuse || metal) Q.Refl = MaterialTexturableReflectance(S, M, PT_BASIC_METAL_BASE_SPECTRUM, P.Lambda, P.TextureUV);
+    if (diffuse || metal)
+        Q.Refl = MaterialTexturableReflectance<MATS == PT_MATS_DIFFUSE>(S, M, PT_BASIC_METAL_BASE_SPECTRUM, P.Lambda,
+                                                                        P.TextureUV);
     if (metal) Q.Aux = MaterialTexturableReflectance(S, M, PT_BASIC_METAL_SPECULAR_SPECTRUM, P.Lambda, P.TextureUV);
     if (trans) {
         pt4 Interior = CauchyEmpiricalIOR(MFloat(S, M, PT_BASIC_TRANSLUCENT_IOR),
@@ -1895,10 +1897,12 @@ hipError_t pt_launch_rounds(const ptd::dscene& S, const ptd::dslots& L, const pt
 // scene's mask is launched.
 uint32_t pt_shade_mats(uint32_t scene_mats)
 {
-    // Diffuse meshes without sky light sampling (the Viking Room, C3): the
-    // lean instantiation, which has no sky lobe and no analytic shapes.
+    // Diffuse meshes without sky light sampling whose textures lie in the
+    // unit square of the atlas (the Viking Room, C3): the lean instantiation,
+    // which has no sky lobe and no analytic shapes and wraps texel
+    // coordinates with two selects (pt_device.hpp Texel).
     if ((scene_mats & ~(uint32_t)PT_MATS_DIFFUSE) == 0) return PT_MATS_DIFFUSE;
-    scene_mats |= PT_MATS_SCENE;
+    scene_mats = (scene_mats & ~(uint32_t)PT_MATS_TEXWRAP) | PT_MATS_SCENE;
     if ((scene_mats & ~(uint32_t)(PT_MATS_DIFFUSE | PT_MATS_SCENE)) == 0) return PT_MATS_DIFFUSE | PT_MATS_SCENE;
     if ((scene_mats & ~(uint32_t)(PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_SCENE)) == 0)
         return PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_SCENE;

@@ -81,6 +81,7 @@ enum : uint32_t {
     PT_MATS_PRIMS = 32,       // some shape is a plane, sphere or cube (else every shape is a mesh instance)
     PT_MATS_SKY = 64,         // SkyboxSamplingProbability != 0 (sky light sampling can be drawn)
     PT_MATS_SCENE = PT_MATS_PRIMS | PT_MATS_SKY,
+    PT_MATS_TEXWRAP = 128,    // some texture's atlas placement lies outside [0, 1] (host mask only: no lean kernel)
 };
 uint32_t pt_shade_mats(uint32_t scene_mats);
 // Preview base-colour tables: the 16 sample constants of ObserveUnderD65

@@ -447,15 +447,25 @@ PT_DEV size_t AtlasIndex(const dscene& S, uint32_t Layer, uint32_t X, uint32_t Y
     return layer + ((size_t)((Y >> 1) * (S.atlas_w >> 2) + (X >> 2)) << 3) + ((Y & 1u) << 2) + (X & 3u);
 }
 
+template <bool UNIT>
 PT_DEV float4 Texel(const dscene& S, uint32_t Layer, int X, int Y)
 {
     if (S.atlas_layers == 0) return make_float4(0, 0, 0, 0);
     int W = (int)S.atlas_w, H = (int)S.atlas_h;
-    // REPEAT wrap.  (Taking the remainder only for coordinates outside
-    // [0, W) measured 1 % slower on C3 shade: the divisor is wave-uniform, so
-    // the remainder is a few VALU, less than the branch's exec handling.)
-    X %= W; if (X < 0) X += W;
-    Y %= H; if (Y < 0) Y += H;
+    // REPEAT wrap.  UNIT: every texture's placement lies in [0, 1] (the
+    // lean shade instantiation, whose scenes the host checked: kernels.hpp
+    // PT_MATS_TEXWRAP), so SampleTexture's coordinates lie in [-1, W] (U in
+    // [0, 1] up to rounding: floor(U * W - 0.5) >= -1, floor(U * W) <= W),
+    // where one add or subtract of W is the remainder -- two selects per axis
+    // instead of a signed integer remainder (about 22 VALU with two
+    // quarter-rate multiplies each, 8 per bilinear sample).
+    if (UNIT) {
+        X = X < 0 ? X + W : X; X = X >= W ? X - W : X;
+        Y = Y < 0 ? Y + H : Y; Y = Y >= H ? Y - H : Y;
+    } else {
+        X %= W; if (X < 0) X += W;
+        Y %= H; if (Y < 0) Y += H;
+    }
     if (Layer >= S.atlas_layers) Layer = S.atlas_layers - 1;
     return S.atlas[AtlasIndex(S, Layer, (uint32_t)X, (uint32_t)Y)];
 }
@@ -463,6 +473,7 @@ PT_DEV float4 Texel(const dscene& S, uint32_t Layer, int X, int Y)
 PT_DEV pt4 f4(float4 a) { return v4(a.x, a.y, a.z, a.w); }
 
 // SampleTexture (scene.glsl.inc:181-205) with software REPEAT filtering.
+template <bool UNIT = false>
 PT_DEV pt4 SampleTexture(const dscene& S, uint32_t Index, pt2 UV)
 {
     const pt_packed_texture T = S.textures[Index];
@@ -470,13 +481,13 @@ PT_DEV pt4 SampleTexture(const dscene& S, uint32_t Index, pt2 UV)
     float V = pt_mix(T.AtlasPlacementMinimum[1], T.AtlasPlacementMaximum[1], pt_fract(UV.y));
     float W = (float)S.atlas_w, H = (float)S.atlas_h;
     if (T.Flags & PT_TEXTURE_FLAG_FILTER_NEAREST)
-        return f4(Texel(S, T.AtlasImageIndex, (int)pt_floor(U * W), (int)pt_floor(V * H)));
+        return f4(Texel<UNIT>(S, T.AtlasImageIndex, (int)pt_floor(U * W), (int)pt_floor(V * H)));
     float Us = U * W - 0.5f, Vs = V * H - 0.5f;
     float Fi = pt_floor(Us), Fj = pt_floor(Vs);
     float A = Us - Fi, B = Vs - Fj;
     int I0 = (int)Fi, J0 = (int)Fj;
-    pt4 T00 = f4(Texel(S, T.AtlasImageIndex, I0, J0)), T10 = f4(Texel(S, T.AtlasImageIndex, I0 + 1, J0));
-    pt4 T01 = f4(Texel(S, T.AtlasImageIndex, I0, J0 + 1)), T11 = f4(Texel(S, T.AtlasImageIndex, I0 + 1, J0 + 1));
+    pt4 T00 = f4(Texel<UNIT>(S, T.AtlasImageIndex, I0, J0)), T10 = f4(Texel<UNIT>(S, T.AtlasImageIndex, I0 + 1, J0));
+    pt4 T01 = f4(Texel<UNIT>(S, T.AtlasImageIndex, I0, J0 + 1)), T11 = f4(Texel<UNIT>(S, T.AtlasImageIndex, I0 + 1, J0 + 1));
     return ((1 - A) * (1 - B)) * T00 + (A * (1 - B)) * T10 + ((1 - A) * B) * T01 + (A * B) * T11;
 }
 
@@ -502,12 +513,13 @@ PT_DEV uint32_t MUint(const dscene& S, uint32_t M, uint32_t A) { return S.materi
 PT_DEV float MFloat(const dscene& S, uint32_t M, uint32_t A) { return pt_u2f(MUint(S, M, A)); }
 PT_DEV pt3 MVec3(const dscene& S, uint32_t M, uint32_t A) { return v3(MFloat(S, M, A), MFloat(S, M, A + 1), MFloat(S, M, A + 2)); }
 
+template <bool UNIT = false>
 PT_DEV pt4 MaterialTexturableReflectance(const dscene& S, uint32_t M, uint32_t A, pt4 Lambda, pt2 UV)
 {
     pt4 Value = SampleParametricSpectrum(MVec3(S, M, A), Lambda);
     uint32_t Tx = MUint(S, M, A + 3);
     if (Tx != TEXTURE_INDEX_NONE) {
-        pt4 T = SampleTexture(S, Tx, UV);
+        pt4 T = SampleTexture<UNIT>(S, Tx, UV);
         Value = Value * SampleParametricSpectrum(v3(T.x, T.y, T.z), Lambda);
     }
     return Value;

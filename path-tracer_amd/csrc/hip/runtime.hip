@@ -638,6 +638,13 @@ static uint32_t SceneMaterialMask(const pt_scene_packs* p)
     for (uint32_t i = 0; i < p->shape_count; i++)
         if (p->shapes[i].Type != PT_SHAPE_TYPE_MESH_INSTANCE) m |= PT_MATS_PRIMS;
     if (!(p->globals->SkyboxSamplingProbability == 0.0f)) m |= PT_MATS_SKY;
+    // The lean instantiation's two-select texel wrap is exact when every
+    // atlas placement lies in [0, 1] (the atlas packer's always do).
+    for (uint32_t i = 0; i < p->texture_count; i++)
+        for (int k = 0; k < 2; k++) {
+            const float a = p->textures[i].AtlasPlacementMinimum[k], b = p->textures[i].AtlasPlacementMaximum[k];
+            if (!((a >= 0.0f) & (a <= 1.0f) & (b >= 0.0f) & (b <= 1.0f))) m |= PT_MATS_TEXWRAP;
+        }
     return m;
 }
 

@@ -1,0 +1,8 @@
+# Two-select texel wrap (in-tree "base") against the integer remainder
+# (build/variants/head.so): C3 / C2 / C5, then the GPU tests.
+set -e
+bash tools/r04/gpu_ab.sh r04_wrap_c3 3 3 head base
+bash tools/r04/gpu_ab.sh r04_wrap_c2 2 2 head base
+STEPS=1 ARGS="--spp 1024" bash tools/r04/gpu_ab.sh r04_wrap_c5 5 1 head base
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r04_wrap_tests.log 2>&1 || { tail -30 gpurun_out/r04_wrap_tests.log; exit 1; }
+tail -2 gpurun_out/r04_wrap_tests.log
