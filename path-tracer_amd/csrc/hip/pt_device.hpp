@@ -47,6 +47,7 @@ struct dscene {
     uint32_t mat_classes;          // shapes use more than one material type: extend classes hits by type
     uint32_t vidx21;               // every vertex index fits 21 bits: hit records carry a face's vertex indices
     float vmf_inv_kappa, vmf_exp_m2k, vmf_norm;   // VmfConstants(g.SkyboxConcentration), set on upload
+    float sky_flat;                // SampleParametricSpectrum((0, 0, 100), L) for any finite L (SkyFlat)
 };
 
 struct ray { pt3 Origin; pt3 Velocity; float Duration; };
@@ -425,6 +426,15 @@ PT_DEV float SampleParametricSpectrum(pt3 B, float L)
     return 0.5f + X / (2.0f * pt_sqrt(1.0f + X * X));
 }
 
+// The untextured sky's spectrum (0, 0, 100) at any finite wavelength:
+// (0 * L + 0) * L + 100 = 100 exactly, so every wavelength gives this value;
+// evaluated once per scene upload with the same pt_fp.h operations.
+PT_HD float SkyFlat()
+{
+    const float X = 100.0f;
+    return 0.5f + X / (2.0f * pt_sqrt(1.0f + X * X));
+}
+
 PT_DEV pt4 SampleParametricSpectrum(pt3 B, pt4 L)
 {
     return v4(SampleParametricSpectrum(B, L.x), SampleParametricSpectrum(B, L.y), SampleParametricSpectrum(B, L.z),
@@ -505,6 +515,9 @@ PT_DEV pt4 SampleSkyboxSpectrum(const dscene& S, pt3 D)
 // SampleSkyboxRadiance (scene.glsl.inc:225-229)
 PT_DEV pt4 SampleSkyboxRadiance(const dscene& S, pt3 D, pt4 Lambda)
 {
+    // Untextured sky: (1 * SampleParametricSpectrum((0, 0, 100), Lambda)) is
+    // the per-scene constant sky_flat at every (finite) wavelength.
+    if (S.g.SkyboxTextureIndex == TEXTURE_INDEX_NONE) return v4s(S.sky_flat) * S.g.SkyboxBrightness;
     pt4 Spectrum = SampleSkyboxSpectrum(S, D);
     return (Spectrum.w * SampleParametricSpectrum(v3(Spectrum.x, Spectrum.y, Spectrum.z), Lambda)) * S.g.SkyboxBrightness;
 }

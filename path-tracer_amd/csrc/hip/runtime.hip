@@ -711,6 +711,7 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
         D.vmf_inv_kappa = K.inv_kappa;
         D.vmf_exp_m2k = K.exp_m2k;
         D.vmf_norm = K.norm;
+        D.sky_flat = ptd::SkyFlat();
     }
     D.textures = s->textures.ptr;
     D.material = s->material.ptr;
