@@ -652,6 +652,12 @@ PT_DEV bool SampleSurfaceIntegrand(const dscene& S, rng& G, pt3 Nrm, pt3 TX, pt3
         }
         if (!ok) return false;
     }
+    if (!(MATS & PT_MATS_SKY)) {
+        // LightProbability = +0 and a finite sky pdf (the host's
+        // PT_MATS_SKY rule): +0 * pdf + 1 * MaterialPDF = MaterialPDF + 0.
+        Probability = MaterialPDF + v4s(0.0f);
+        return true;
+    }
     pt4 SkyboxPDF = v4s(VonMisesFisherPDF(S.g.SkyboxConcentration, vmf_consts{S.vmf_inv_kappa, S.vmf_exp_m2k, S.vmf_norm},
                                           Mu, In));
     Probability = LightProbability * SkyboxPDF + (1 - LightProbability) * MaterialPDF;

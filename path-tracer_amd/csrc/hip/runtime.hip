@@ -637,7 +637,24 @@ static uint32_t SceneMaterialMask(const pt_scene_packs* p)
     if ((m & PT_MATS_TRANSLUCENT) || p->globals->SceneScatterRate > 0.0f) m |= PT_MATS_SCATTER;
     for (uint32_t i = 0; i < p->shape_count; i++)
         if (p->shapes[i].Type != PT_SHAPE_TYPE_MESH_INSTANCE) m |= PT_MATS_PRIMS;
-    if (!(p->globals->SkyboxSamplingProbability == 0.0f)) m |= PT_MATS_SKY;
+    // PT_MATS_SKY clear: the light is never chosen and its pdf term is an
+    // exact +0, so the shade kernel drops the sky lobe and the sky pdf
+    // (SampleSurfaceIntegrand).  That needs SkyboxSamplingProbability == +0
+    // (bit pattern 0: LP * pdf is then +0) and a finite pdf for every
+    // direction: the constant 1/(4 pi) below PT_EPSILON, else a finite norm,
+    // Kappa <= 1000 and |SkyboxMeanDirection|^2 <= 1.01 (so Kappa (Mu.In - 1)
+    // stays far below exp's overflow).
+    {
+        const pt_packed_scene_globals& G = *p->globals;
+        const float K = G.SkyboxConcentration;
+        const float* D = G.SkyboxMeanDirection;
+        const float norm = ptd::VmfConstants(K).norm;
+        const bool pdf_finite = (K < PT_EPSILON) || (std::isfinite(norm) && K <= 1000.0f &&
+                                                     D[0] * D[0] + D[1] * D[1] + D[2] * D[2] <= 1.01f);
+        uint32_t ssp;
+        std::memcpy(&ssp, &G.SkyboxSamplingProbability, 4);
+        if (ssp != 0u || !pdf_finite) m |= PT_MATS_SKY;
+    }
     // The lean instantiation's two-select texel wrap is exact when every
     // atlas placement lies in [0, 1] (the atlas packer's always do).
     for (uint32_t i = 0; i < p->texture_count; i++)
