@@ -262,6 +262,56 @@ int                ptRenderFrame(pt_device* device, pt_basic_renderer* renderer,
 int                ptReadBasicRendererState(pt_device* device, pt_basic_renderer* renderer, pt_pixel_state* out);
 int                ptReadBasicRendererStreamState(pt_device* device, pt_basic_renderer* renderer, uint32_t stream,
                                                   pt_pixel_state* out);
+/* Resume (no reference counterpart; the reference restarts paths on Reset,
+ * basic_scatter.glsl:330-336): restores the live path of every owned pixel
+ * of stream 0 (or `stream`) from `in` (width*height states in image order, as
+ * ptReadBasicRendererState returned them between rounds; other pixels are not
+ * read): the next ray and the path record (lambda0, throughput, probability,
+ * active shapes).  The trace record is not restored -- the next Run traces
+ * the restored ray before it scatters, so it is not needed; the readback shows
+ * a miss until then.  With the accumulator (ptWriteSampleBuffer) and
+ * FrameIndex restored too, the following Runs equal the uninterrupted
+ * render's bit for bit.  Fails, writing nothing, if a sample is non-zero (a
+ * live path's is 0 between rounds), a lambda0 lies outside [0, 1) or an
+ * active entry is neither 0xFFFF nor a shape of the scene.  Synchronises. */
+int                ptWriteBasicRendererState(pt_device* device, pt_basic_renderer* renderer, const pt_pixel_state* in);
+int                ptWriteBasicRendererStreamState(pt_device* device, pt_basic_renderer* renderer, uint32_t stream,
+                                                   const pt_pixel_state* in);
+/* A path stream's own accumulator (width*height*4 floats, as
+ * ptReadSampleBuffer): with one stream it is the sample buffer; with several,
+ * the per-stream sums ptMergeBasicRendererStreams adds up.  Saving and
+ * restoring every stream's accumulator and state resumes a multi-stream
+ * render bit for bit. */
+int                ptReadBasicRendererStreamAccumulator(pt_device* device, pt_basic_renderer* renderer, uint32_t stream,
+                                                        float* rgba);
+int                ptWriteBasicRendererStreamAccumulator(pt_device* device, pt_basic_renderer* renderer,
+                                                         uint32_t stream, const float* rgba);
+
+/* Diagnostic: the shade variant the renderer runs (chosen on the host from
+ * the scene's packs at ptUpdateScene and from the renderer's options; no
+ * effect on results).  Mask bits: material types present, a scattering
+ * medium, analytic shapes, sky light sampling that matters (the host cannot
+ * prove SkyboxSamplingProbability * pdf an exact +0), texture placements
+ * outside the unit square. */
+enum {
+    PT_SHADE_DIFFUSE     = 1,
+    PT_SHADE_METAL       = 2,
+    PT_SHADE_TRANSLUCENT = 4,
+    PT_SHADE_SCATTER     = 8,
+    PT_SHADE_OPENPBR     = 16,
+    PT_SHADE_PRIMS       = 32,
+    PT_SHADE_SKY         = 64,
+    PT_SHADE_TEXWRAP     = 128,
+};
+typedef struct pt_shade_info {
+    uint32_t scene_mask;        /* PT_SHADE_* of the scene as the renderer shades it */
+    uint32_t kernel_mask;       /* the instantiation launched: the smallest superset built
+                                   (PT_SHADE_DIFFUSE alone = the lean diffuse-mesh kernel) */
+    uint32_t completion_queue;  /* 1: completed paths restart through the block's queue */
+    uint32_t grey_records;      /* 1: live paths keep one Probability float and no stack
+                                   (as of the last Reset / Run / state write) */
+} pt_shade_info;
+int                ptGetBasicRendererShadeInfo(pt_basic_renderer* renderer, pt_shade_info* info);
 
 /* Editor preview (preview_render.glsl:96-178): one primary ray per pixel of
  * RenderSizeX x RenderSizeY through the same Trace() as the integrator.

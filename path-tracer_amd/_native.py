@@ -39,6 +39,16 @@ class pt_scene_packs(C.Structure):
     ]
 
 
+class pt_shade_info(C.Structure):
+    """pt_shade_info (include/pt_api.h): the shade variant a renderer runs."""
+    _fields_ = [("scene_mask", C.c_uint32), ("kernel_mask", C.c_uint32), ("completion_queue", C.c_uint32),
+                ("grey_records", C.c_uint32)]
+
+
+SHADE_DIFFUSE, SHADE_METAL, SHADE_TRANSLUCENT, SHADE_SCATTER = 1, 2, 4, 8
+SHADE_OPENPBR, SHADE_PRIMS, SHADE_SKY, SHADE_TEXWRAP = 16, 32, 64, 128
+
+
 class pt_basic_renderer_params(C.Structure):
     _fields_ = [
         ("FrameIndex", C.c_uint32),
@@ -234,6 +244,11 @@ HIP_API = {
     "ptMergeBasicRendererStreams": (_i32, [_vp, _vp]),
     "ptBasicRendererStreams": (_u32, [_vp]),
     "ptReadBasicRendererStreamState": (_i32, [_vp, _vp, _u32, _vp]),
+    "ptWriteBasicRendererState": (_i32, [_vp, _vp, _vp]),
+    "ptWriteBasicRendererStreamState": (_i32, [_vp, _vp, _u32, _vp]),
+    "ptReadBasicRendererStreamAccumulator": (_i32, [_vp, _vp, _u32, _fptr]),
+    "ptWriteBasicRendererStreamAccumulator": (_i32, [_vp, _vp, _u32, _fptr]),
+    "ptGetBasicRendererShadeInfo": (_i32, [_vp, C.POINTER(pt_shade_info)]),
     "ptDestroyBasicRenderer": (None, [_vp, _vp]),
     "ptBasicRendererParams": (C.POINTER(pt_basic_renderer_params), [_vp]),
     "ptResetBasicRenderer": (_i32, [_vp, _vp]),

@@ -711,10 +711,27 @@ PT_DEV pt3 EscapeContribution(const dscene& S, pt3 V, pt4 Lambda, pt4 Throughput
 // `act_none`: the slot's stored active-shape stack is already empty (all
 // four entries NONE), as a new path's is, so its 8-byte record is not
 // rewritten (a partial-line store for every completed path otherwise).
+//
+// GreyRecord: when the renderer's shade mask has no translucent and no
+// OpenPBR material (pt_grey_mats), every factor Scatter multiplies into a
+// path's Probability is the same for the four wavelengths -- the diffuse and
+// metal pdfs are scalars (basic_diffuse.glsl.inc:30-33, basic_metal.glsl.inc),
+// the sky pdf too, the medium density of the vacuum-or-scene-fog medium is
+// v4(SceneScatterRate) based (basic_scatter.glsl:137-163), the roulette
+// factor is a scalar (:295-298) -- and a new path starts at vec4(1); so the
+// four components are the same bits, and the slot stores one float
+// (L.prob1).  The active-shape stack can only grow on a refraction into a
+// shape (In.z * Out.z < 0 with Out.z > 0, :266-282), which needs a
+// translucent (or OpenPBR) BSDF: diffuse / metal directions have In.z >= 0,
+// a sky sample below the surface ends the path, and a non-real hit seen from
+// outside cannot occur with an empty stack; so it stays empty and is neither
+// read nor written.  The host switches a renderer's live paths between the
+// forms (pt_launch_grey_convert) when its shade mask changes.
 PT_DEV void StorePathVertex(const dslots& L, uint32_t s, const path& P, bool act_none = false)
 {
     L.thr[s] = make_float4(P.Throughput.x, P.Throughput.y, P.Throughput.z, P.Throughput.w);
-    L.prob[s] = make_float4(P.Probability.x, P.Probability.y, P.Probability.z, P.Probability.w);
+    if (L.prob1) L.prob1[s] = P.Probability.x;
+    else L.prob[s] = make_float4(P.Probability.x, P.Probability.y, P.Probability.z, P.Probability.w);
     L.lam[s] = P.Lambda0;
     if (!act_none) L.act[s] = make_uint2((P.Active[1] << 16) | P.Active[0], (P.Active[3] << 16) | P.Active[2]);
 }
@@ -1018,6 +1035,23 @@ __global__ __launch_bounds__(256) void raygen_kernel(dscene S, dslots L, dframe 
     TileOrderStoreRay(L, s, valid, O, V, L.pos[s] & 255u);
 }
 
+// State write (ptWriteBasicRendererState): the restored rays of one tile,
+// given by slot, go to their TileOrder positions like a shade's new rays;
+// every position of the tile gets a miss record (no trace of the restored
+// rays exists until the next extend, which overwrites it).  The order does
+// not change any result (TileOrder).
+__global__ __launch_bounds__(256) void restore_rays_kernel(dslots L, dframe F, const float4* rays, uint32_t tile0)
+{
+    const uint32_t s = (tile0 + blockIdx.x) * 256 + threadIdx.x;
+    uint32_t x, y;
+    const bool valid = SlotPixel(F, s, x, y);
+    const float4 r = rays[s - tile0 * 256];
+    const uint32_t key = TileOrderKey(valid, UnpackUnitVector(__float_as_uint(r.w)));
+    L.hit[s] = make_float4(0.0f, __uint_as_float(SHAPE_INDEX_NONE), 0.0f, 0.0f);
+    L.uv[s] = make_float2(0.0f, 0.0f);
+    TileOrderStoreKeyed(L, s, key, r, 0u);
+}
+
 // Ray sources of the extend kernel: the renderer's slots, or the arrays of
 // the ray-query API.
 struct ray_source_slots {
@@ -1271,6 +1305,38 @@ __global__ __launch_bounds__(256) void merge_streams_kernel(float4* accum, float
     }
 }
 
+// Record forms of the live paths (GreyRecord, StorePathVertex).  Only slots
+// of pixels inside the image hold paths.
+__global__ __launch_bounds__(256) void grey_check_kernel(dslots L, dframe F, uint32_t* count)
+{
+    const uint32_t s = blockIdx.x * 256 + threadIdx.x;
+    uint32_t x, y;
+    bool bad = false;
+    if (s < L.n && SlotPixel(F, s, x, y)) {
+        const float4 p = L.prob[s];
+        const uint2 a = L.act[s];
+        const uint32_t b = __float_as_uint(p.x);
+        bad = b != __float_as_uint(p.y) || b != __float_as_uint(p.z) || b != __float_as_uint(p.w) ||
+              (a.x & a.y) != 0xFFFFFFFFu;
+    }
+    const uint64_t m = __ballot(bad);
+    if ((threadIdx.x & 63u) == 0 && m) atomicAdd(count, (uint32_t)__popcll(m));
+}
+
+__global__ __launch_bounds__(256) void grey_convert_kernel(dslots L, dframe F, float* prob1, bool to_grey)
+{
+    const uint32_t s = blockIdx.x * 256 + threadIdx.x;
+    uint32_t x, y;
+    if (s >= L.n || !SlotPixel(F, s, x, y)) return;
+    if (to_grey) {
+        prob1[s] = L.prob[s].x;
+    } else {
+        const float c = prob1[s];
+        L.prob[s] = make_float4(c, c, c, c);
+        L.act[s] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+    }
+}
+
 __global__ __launch_bounds__(256) void zero_unowned_kernel(float4* accum, uint32_t width, uint32_t height,
                                                            uint32_t rank, uint32_t nranks)
 {
@@ -1409,12 +1475,21 @@ PT_DEV void ShadeSlot(const dscene& S, const dslots& L, const dframe& F, const d
         rng G;
         G.State = pt_seed(x, y, StreamSeed(Pm.seed, stream));
 
-        // LoadPath (basic.glsl.inc:159-198)
+        // LoadPath (basic.glsl.inc:159-198).  Grey record form (StorePathVertex):
+        // one Probability float, and the empty stack without a load.
+        const bool grey = pt_grey_mats(MATS) && L.prob1 != nullptr;
         path P;
-        float4 thr = L.thr[s], prob = L.prob[s];
-        uint2 act = L.act[s];
+        float4 thr = L.thr[s];
+        uint2 act;
+        if (grey) {
+            P.Probability = v4s(L.prob1[s]);
+            act = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+        } else {
+            float4 prob = L.prob[s];
+            P.Probability = v4(prob.x, prob.y, prob.z, prob.w);
+            act = L.act[s];
+        }
         P.Throughput = v4(thr.x, thr.y, thr.z, thr.w);
-        P.Probability = v4(prob.x, prob.y, prob.z, prob.w);
         P.Sample = v3s(0.0f);          // always 0 between rounds (StorePathVertex)
         P.Lambda0 = L.lam[s];
         P.Active[0] = act.x & 0xFFFF; P.Active[1] = act.x >> 16;
@@ -1464,9 +1539,13 @@ PT_DEV void ShadeSlot(const dscene& S, const dslots& L, const dframe& F, const d
             // is unchanged; the active-shape stack is written when it moved.
             ShadeMark(SM_CONTINUE);
             L.thr[s] = make_float4(P.Throughput.x, P.Throughput.y, P.Throughput.z, P.Throughput.w);
-            L.prob[s] = make_float4(P.Probability.x, P.Probability.y, P.Probability.z, P.Probability.w);
-            uint2 na = make_uint2((P.Active[1] << 16) | P.Active[0], (P.Active[3] << 16) | P.Active[2]);
-            if ((na.x != act.x) | (na.y != act.y)) L.act[s] = na;
+            if (grey) {
+                L.prob1[s] = P.Probability.x;
+            } else {
+                L.prob[s] = make_float4(P.Probability.x, P.Probability.y, P.Probability.z, P.Probability.w);
+                uint2 na = make_uint2((P.Active[1] << 16) | P.Active[0], (P.Active[3] << 16) | P.Active[2]);
+                if ((na.x != act.x) | (na.y != act.y)) L.act[s] = na;
+            }
         } else {
             ShadeMark(SM_COMPLETED);
             completed = true;
@@ -1793,6 +1872,29 @@ hipError_t pt_launch_merge_streams(float4* accum, float4* accx, uint32_t width, 
     if (streams <= 1 || width == 0 || height == 0) return hipSuccess;
     hipLaunchKernelGGL(ptd::merge_streams_kernel, dim3(Blocks(width), height < 32768u ? height : 32768u), dim3(256), 0,
                        st, accum, accx, width, height, rank, nranks, streams);
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_restore_rays(const ptd::dslots& L, const ptd::dframe& F, const float4* rays, uint32_t tile0,
+                                  uint32_t tiles, hipStream_t st)
+{
+    if (tiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(ptd::restore_rays_kernel, dim3(tiles), dim3(256), 0, st, L, F, rays, tile0);
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_grey_check(const ptd::dslots& L, const ptd::dframe& F, uint32_t* count, hipStream_t st)
+{
+    if (L.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(ptd::grey_check_kernel, dim3(Blocks(L.n)), dim3(256), 0, st, L, F, count);
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_grey_convert(const ptd::dslots& L, const ptd::dframe& F, float* prob1, bool to_grey,
+                                  hipStream_t st)
+{
+    if (L.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(ptd::grey_convert_kernel, dim3(Blocks(L.n)), dim3(256), 0, st, L, F, prob1, to_grey);
     return hipGetLastError();
 }
 

@@ -20,6 +20,8 @@ struct dslots {
     float2* uv;         // compact hit: coords.y, coords.z
     float4* thr;        // throughput[4]
     float4* prob;       // probability[4]
+    float* prob1;       // grey record form (non-null): the path's Probability, whose four components
+                        // are equal, as one float; prob and act are then not read (GreyRecord, kernels.hip)
     float* lam;         // normalized lambda0 (a live path's Sample is always 0: StorePathVertex)
     uint2* act;         // active-shape stack (2 x u16 pairs)
     uint16_t* pos;      // per slot: position of its current ray (high byte) and of
@@ -84,6 +86,20 @@ enum : uint32_t {
     PT_MATS_TEXWRAP = 128,    // some texture's atlas placement lies outside [0, 1] (host mask only: no lean kernel)
 };
 uint32_t pt_shade_mats(uint32_t scene_mats);
+// Grey record form (kernels.hip GreyRecord): the shade mask keeps every path's
+// Probability wavelength-uniform and its active-shape stack empty.
+constexpr bool pt_grey_mats(uint32_t shade_mats) { return !(shade_mats & (PT_MATS_TRANSLUCENT | PT_MATS_OPENPBR)); }
+// Record-form conversions of a renderer's live paths (between rounds):
+// counts the valid slots whose Probability components differ or whose stack
+// is not empty (a path that cannot take the grey form); converts every valid
+// slot's record to the grey form (to_grey) or back to the four-float form.
+// State write: rays[i] = the restored ray of slot tile0 * 256 + i, for
+// `tiles` tiles; stored at their TileOrder positions, every hit a miss.
+hipError_t pt_launch_restore_rays(const ptd::dslots& L, const ptd::dframe& F, const float4* rays, uint32_t tile0,
+                                  uint32_t tiles, hipStream_t st);
+hipError_t pt_launch_grey_check(const ptd::dslots& L, const ptd::dframe& F, uint32_t* count, hipStream_t st);
+hipError_t pt_launch_grey_convert(const ptd::dslots& L, const ptd::dframe& F, float* prob1, bool to_grey,
+                                  hipStream_t st);
 // Preview base-colour tables: the 16 sample constants of ObserveUnderD65
 // (preview.hip), filled once per preview context.
 constexpr uint32_t PT_OBSERVE_TABLE_FLOATS = 16 * 5;

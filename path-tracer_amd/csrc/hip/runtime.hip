@@ -160,6 +160,10 @@ struct pt_basic_renderer {
     uint32_t tiles_x = 0;
     ptd::dslots slots{};
     dbuf<float4> ray, hit, thr, prob;
+    dbuf<float> prob1;                  // grey record form's Probability (kernels.hip StorePathVertex)
+    bool grey = false;                  // the live paths are in the grey record form (slots.prob1 set)
+    bool grey_blocked = false;          // some live path cannot take it (until the next Reset / state write)
+    dbuf<uint32_t> grey_count;          // pt_launch_grey_check's result word
     dbuf<float> lam;                    // lambda0 per slot (Sample is 0 between rounds)
     dbuf<float2> uv;
     dbuf<uint2> act;
@@ -188,6 +192,8 @@ struct pt_comm {
     double timeout_s = 600.0;     // ptCommSetTimeout
     bool aborted = false;
     int* flag = nullptr;          // device word of the collective argument check (CommAgree)
+    int* host_flag = nullptr;     // its pinned host copy: the readback stays an asynchronous copy
+                                  // that DeviceWait polls, and outlives a wait that times out
 };
 
 namespace {
@@ -494,6 +500,10 @@ void ptDestroyDevice(pt_device* d)
     if (!d) return;
     (void)hipSetDevice(d->id);
     (void)DeviceWait(d);
+    // Communicators outliving their device: detached (ptCommDestroy still
+    // releases them; every exchange on them fails).
+    for (pt_comm* c : d->comms) c->dev = nullptr;
+    d->comms.clear();
     for (auto& ep : d->pending) { (void)hipEventDestroy(ep.a); (void)hipEventDestroy(ep.b); }
     for (auto& ep : d->free_events) { (void)hipEventDestroy(ep.a); (void)hipEventDestroy(ep.b); }
     (void)hipStreamDestroy(d->stream);
@@ -889,7 +899,8 @@ pt_basic_renderer* ptCreateBasicRendererStreams(pt_device* d, pt_scene* s, pt_sa
     if (n > 0xFFFFFFFFull / 2) { SetError("too many slots"); delete r; return nullptr; }
     uint32_t ns = (uint32_t)n;
     bool ok = r->ray.alloc(ns) == hipSuccess && r->hit.alloc(ns) == hipSuccess && r->thr.alloc(ns) == hipSuccess &&
-              r->prob.alloc(ns) == hipSuccess && r->lam.alloc(ns) == hipSuccess && r->uv.alloc(ns) == hipSuccess &&
+              r->prob.alloc(ns) == hipSuccess && r->prob1.alloc(ns) == hipSuccess && r->grey_count.alloc(1) == hipSuccess &&
+              r->lam.alloc(ns) == hipSuccess && r->uv.alloc(ns) == hipSuccess &&
               r->act.alloc(ns) == hipSuccess && r->pos.alloc(ns) == hipSuccess && r->slotof.alloc(ns) == hipSuccess &&
               r->outcome.alloc((size_t)(ns / 256) * 4 * ptd::PT_OUTCOME_CLASSES + 1) == hipSuccess &&
               r->tilecost.alloc((size_t)(ns / 256) * 4 + 1) == hipSuccess && r->order.alloc(ns / 256 + 1) == hipSuccess &&
@@ -901,6 +912,7 @@ pt_basic_renderer* ptCreateBasicRendererStreams(pt_device* d, pt_scene* s, pt_sa
     if (ok && ns) {
         ok = hipMemset(r->ray.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->hit.ptr, 0, (size_t)ns * 16) == hipSuccess &&
              hipMemset(r->thr.ptr, 0, (size_t)ns * 16) == hipSuccess && hipMemset(r->prob.ptr, 0, (size_t)ns * 16) == hipSuccess &&
+             hipMemset(r->prob1.ptr, 0, (size_t)ns * 4) == hipSuccess &&
              hipMemset(r->lam.ptr, 0, (size_t)ns * 4) == hipSuccess && hipMemset(r->uv.ptr, 0, (size_t)ns * 8) == hipSuccess &&
              hipMemset(r->act.ptr, 0, (size_t)ns * 8) == hipSuccess && hipMemset(r->done.ptr, 0, (size_t)(ns / 64 + 1) * 4) == hipSuccess &&
              hipMemset(r->outcome.ptr, 0, ((size_t)(ns / 256) * 4 * ptd::PT_OUTCOME_CLASSES + 1) * 8) == hipSuccess;
@@ -917,7 +929,8 @@ pt_basic_renderer* ptCreateBasicRendererStreams(pt_device* d, pt_scene* s, pt_sa
     }
     if (!ok) {
         SetError("renderer slot allocation failed (%u slots)", ns);
-        r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->lam.release(); r->uv.release(); r->act.release();
+        r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->prob1.release(); r->grey_count.release();
+        r->lam.release(); r->uv.release(); r->act.release();
         r->pos.release(); r->slotof.release(); r->outcome.release(); r->tilecost.release(); r->order.release();
         r->done.release(); r->accx.release();
         delete r;
@@ -979,7 +992,8 @@ void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
 {
     if (!r) return;
     if (d) { (void)hipSetDevice(d->id); (void)DeviceWait(d); }
-    r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->lam.release();
+    r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->prob1.release(); r->grey_count.release();
+    r->lam.release();
     r->uv.release(); r->act.release(); r->pos.release(); r->slotof.release(); r->outcome.release();
     r->tilecost.release(); r->order.release();
     r->done.release();
@@ -991,12 +1005,62 @@ void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
 pt_basic_renderer_params* ptBasicRendererParams(pt_basic_renderer* r) { return r ? &r->params : nullptr; }
 uint32_t ptBasicRendererSlotCount(pt_basic_renderer* r) { return r ? r->slots.n : 0; }
 
+// Material mask the renderer shades with (shade / round instantiation): the
+// scene's OpenPBR shapes, and the media they bring, join it only when OpenPBR
+// shading is enabled (ptSetBasicRendererOpenPBR); otherwise their hits end
+// the path as in the reference.
+static uint32_t ShadeMats(const pt_basic_renderer* r)
+{
+    uint32_t m = r->scene->mats;
+    if (!(m & PT_MATS_OPENPBR)) return m;
+    if (!r->openpbr) return m & ~(uint32_t)PT_MATS_OPENPBR;
+    return m | PT_MATS_SCATTER;
+}
+
+// The record form of the renderer's live paths (GreyRecord, kernels.hip
+// StorePathVertex): grey while the shade mask keeps every Probability
+// wavelength-uniform and every active-shape stack empty.  A mask change
+// between rounds (a scene update without Reset, ptSetBasicRendererOpenPBR)
+// converts the live paths: to the four-float form always; to the grey form
+// only if every live path satisfies its invariants (checked on the device:
+// paths that crossed into a glass keep a non-empty stack), else the renderer
+// stays in the four-float form until the next Reset or state write.
+static int SyncRecordForm(pt_device* d, pt_basic_renderer* r)
+{
+    const bool want = pt_grey_mats(ShadeMats(r));
+    if (want != r->grey && r->slots.n) {
+        const ptd::dframe F = Frame(r);
+        if (!want) {
+            PT_HIP(pt_launch_grey_convert(r->slots, F, r->prob1.ptr, false, d->stream));
+            r->grey = false;
+        } else if (!r->grey_blocked) {
+            PT_HIP(hipMemsetAsync(r->grey_count.ptr, 0, sizeof(uint32_t), d->stream));
+            PT_HIP(pt_launch_grey_check(r->slots, F, r->grey_count.ptr, d->stream));
+            PT_WAIT(d);
+            uint32_t bad = 0;
+            PT_HIP(hipMemcpy(&bad, r->grey_count.ptr, sizeof(bad), hipMemcpyDeviceToHost));
+            if (bad == 0) {
+                PT_HIP(pt_launch_grey_convert(r->slots, F, r->prob1.ptr, true, d->stream));
+                r->grey = true;
+            } else {
+                r->grey_blocked = true;
+            }
+        }
+    }
+    r->slots.prob1 = r->grey ? r->prob1.ptr : nullptr;
+    return 0;
+}
+
 // ResetBasicRenderer (basic.cpp:285-304)
 int ptResetBasicRenderer(pt_device* d, pt_basic_renderer* r)
 {
     if (!d) { SetError("null device"); return -1; }
     if (CheckReady(r) != 0) return -1;
     PT_HIP(hipSetDevice(d->id));
+    // Every live path is replaced: the record form follows the shade mask.
+    r->grey = pt_grey_mats(ShadeMats(r));
+    r->grey_blocked = false;
+    r->slots.prob1 = r->grey ? r->prob1.ptr : nullptr;
     event_pair ep{};
     if (int e = BeginTimed(d, PT_KERNEL_RAYGEN, ep)) return e;
     PT_HIP(pt_launch_raygen(r->scene->d, r->slots, Frame(r), Params(r, r->params.FrameIndex), d->stream));
@@ -1011,17 +1075,6 @@ int ptResetBasicRenderer(pt_device* d, pt_basic_renderer* r)
 // at once -- a rank's share of a strongly scaled frame -- and the scene needs
 // no spilled stack (renderer mode 1); mode 0 never fuses, mode 2 fuses
 // whenever the kernel applies (tests and A/B).
-// Material mask the renderer shades with (shade / round instantiation): the
-// scene's OpenPBR shapes, and the media they bring, join it only when OpenPBR
-// shading is enabled (ptSetBasicRendererOpenPBR); otherwise their hits end
-// the path as in the reference.
-static uint32_t ShadeMats(const pt_basic_renderer* r)
-{
-    uint32_t m = r->scene->mats;
-    if (!(m & PT_MATS_OPENPBR)) return m;
-    if (!r->openpbr) return m & ~(uint32_t)PT_MATS_OPENPBR;
-    return m | PT_MATS_SCATTER;
-}
 
 // Completion queue of the shade kernel (kernels.hip ShadeTile): worth its
 // barriers when paths also end at surfaces -- sky light sampling (a sample
@@ -1052,6 +1105,7 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
     if (CheckReady(r) != 0) return -1;
     PT_HIP(hipSetDevice(d->id));
     if (int e = EnsureSpill(r)) return e;
+    if (int e = SyncRecordForm(d, r)) return e;
     r->params.FrameIndex += 1;
     ptd::dparams P = Params(r, r->params.FrameIndex);
     ptd::dframe F = Frame(r);
@@ -1098,6 +1152,7 @@ static int RunRounds(pt_device* d, pt_basic_renderer* r, uint64_t k)
     if (B > 1) {
         PT_HIP(hipSetDevice(d->id));
         if (int e = EnsureSpill(r)) return e;
+        if (int e = SyncRecordForm(d, r)) return e;
         if (pt_rounds_available(r->slots)) {
             const ptd::dframe F = Frame(r);
             while (k > 0) {
@@ -1185,7 +1240,11 @@ int ptGetStats(pt_device* d, pt_basic_renderer* r, uint64_t* rays, uint64_t* sam
 // never longer than the rounds that could not reach the target even if every
 // slot completed a path each round, or than 90 % of the rounds the last
 // batch's completion rate predicts, and within the last 16 predicted rounds
-// only the former -- so the frame ends at the reference's round.
+// only the former.  So the frame ends at the reference's round (the first
+// whose total reaches the target) unless the completion rate rises by more
+// than 1/0.9 - 1 = 11 % within one rate-sized batch; the rate of a frame
+// past its first rounds moves by well under 1 % per batch (the C3 1024-spp
+// frame ends at the reference's round: tests/test_gpu_coverage.py).
 int ptRenderFrame(pt_device* d, pt_basic_renderer* r, uint64_t target_samples, uint32_t max_rounds,
                   uint32_t* rounds_out, uint64_t* samples_out)
 {
@@ -1251,7 +1310,14 @@ int ptReadBasicRendererStreamState(pt_device* d, pt_basic_renderer* r, uint32_t 
     }
     PT_HIP(hipMemcpy(ray.data(), r->ray.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
     PT_HIP(hipMemcpy(thr.data(), r->thr.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
-    PT_HIP(hipMemcpy(prob.data(), r->prob.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
+    if (r->grey) {
+        // Grey record form: the one stored Probability is all four components.
+        std::vector<float> p1(n);
+        PT_HIP(hipMemcpy(p1.data(), r->prob1.ptr, (size_t)n * 4, hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < n; i++) prob[i] = make_float4(p1[i], p1[i], p1[i], p1[i]);
+    } else {
+        PT_HIP(hipMemcpy(prob.data(), r->prob.ptr, (size_t)n * 16, hipMemcpyDeviceToHost));
+    }
     PT_HIP(hipMemcpy(lam.data(), r->lam.ptr, (size_t)n * 4, hipMemcpyDeviceToHost));
     PT_HIP(hipMemcpy(act.data(), r->act.ptr, (size_t)n * 8, hipMemcpyDeviceToHost));
     PT_HIP(hipMemcpy(pos.data(), r->pos.ptr, (size_t)n * 2, hipMemcpyDeviceToHost));
@@ -1286,6 +1352,134 @@ int ptReadBasicRendererStreamState(pt_device* d, pt_basic_renderer* r, uint32_t 
 int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state* out)
 {
     return ptReadBasicRendererStreamState(d, r, 0, out);
+}
+
+// Resume: the live path of every owned pixel of one stream from
+// a saved pt_pixel_state (what ptReadBasicRendererStreamState returned between
+// rounds).  Restored: the next ray (origin, packed velocity) and the path
+// record (basic.glsl.inc:159-198: lambda0, throughput, probability, active
+// stack).  Not restored: the trace record -- each round traces before it
+// scatters (basic_trace.glsl then basic_scatter.glsl), so the next Run's
+// extend replaces it before anything reads it; until then the readback
+// reports a miss.  Sample must be 0: a live path's Sample is 0 between rounds
+// (StorePathVertex, kernels.hip).  Checked before anything is written: every
+// active-stack entry is 0xFFFF or a shape of the scene, lambda0 lies in
+// [0, 1).
+int ptWriteBasicRendererStreamState(pt_device* d, pt_basic_renderer* r, uint32_t stream, const pt_pixel_state* in)
+{
+    if (!d || !in) { SetError("null argument"); return -1; }
+    if (CheckReady(r) != 0) return -1;
+    if (stream >= r->streams) { SetError("stream %u >= the renderer's %u streams", stream, r->streams); return -1; }
+    const uint32_t W = r->buffer->width, H = r->buffer->height;
+    const uint32_t shapes = r->scene->d.g.ShapeCount;
+    const uint32_t T = r->stream_tiles, s0 = stream * T * 256;
+    std::vector<float4> ray((size_t)T * 256), thr((size_t)T * 256), prob((size_t)T * 256);
+    std::vector<float> lam((size_t)T * 256);
+    std::vector<uint2> act((size_t)T * 256);
+    for (uint32_t i = 0; i < T * 256; i++) {
+        const uint32_t t = i >> 8, l = i & 255u, k = t / r->tiles_x, tx = t - k * r->tiles_x;
+        const uint32_t x = tx * 16 + (l & 15u), y = (r->rank + k * r->nranks) * 16 + (l >> 4);
+        ray[i] = make_float4(0, 0, 0, 0);
+        thr[i] = prob[i] = make_float4(0, 0, 0, 0);
+        lam[i] = 0.0f;
+        act[i] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+        if (x >= W || y >= H) continue;
+        const pt_pixel_state& S = in[(size_t)y * W + x];
+        if (S.sample[0] != 0.0f || S.sample[1] != 0.0f || S.sample[2] != 0.0f) {
+            SetError("pixel (%u, %u): a live path's sample is 0 between rounds", x, y);
+            return -1;
+        }
+        if (!(S.lambda0 >= 0.0f && S.lambda0 < 1.0f)) {
+            SetError("pixel (%u, %u): lambda0 %g outside [0, 1)", x, y, (double)S.lambda0);
+            return -1;
+        }
+        const uint32_t e[4] = {S.active01 & 0xFFFFu, S.active01 >> 16, S.active23 & 0xFFFFu, S.active23 >> 16};
+        for (uint32_t v : e)
+            if (v != 0xFFFFu && v >= shapes) {
+                SetError("pixel (%u, %u): active shape %u >= the scene's %u shapes", x, y, v, shapes);
+                return -1;
+            }
+        float w;
+        std::memcpy(&w, &S.packed_velocity, 4);
+        ray[i] = make_float4(S.origin[0], S.origin[1], S.origin[2], w);
+        thr[i] = make_float4(S.throughput[0], S.throughput[1], S.throughput[2], S.throughput[3]);
+        prob[i] = make_float4(S.probability[0], S.probability[1], S.probability[2], S.probability[3]);
+        lam[i] = S.lambda0;
+        act[i] = make_uint2(S.active01, S.active23);
+    }
+    PT_HIP(hipSetDevice(d->id));
+    // The written records are four-float ones: the other streams' live paths
+    // leave the grey form too; the next Run converts back when it can.
+    if (r->grey) PT_HIP(pt_launch_grey_convert(r->slots, Frame(r), r->prob1.ptr, false, d->stream));
+    r->grey = false;
+    r->grey_blocked = false;
+    r->slots.prob1 = nullptr;
+    PT_WAIT(d);
+    const size_t n = (size_t)T * 256;
+    PT_HIP(hipMemcpy(r->thr.ptr + s0, thr.data(), n * 16, hipMemcpyHostToDevice));
+    PT_HIP(hipMemcpy(r->prob.ptr + s0, prob.data(), n * 16, hipMemcpyHostToDevice));
+    PT_HIP(hipMemcpy(r->lam.ptr + s0, lam.data(), n * 4, hipMemcpyHostToDevice));
+    PT_HIP(hipMemcpy(r->act.ptr + s0, act.data(), n * 8, hipMemcpyHostToDevice));
+    dbuf<float4> stage;
+    hipError_t e = stage.upload(ray.data(), n);
+    if (e == hipSuccess) e = pt_launch_restore_rays(r->slots, Frame(r), stage.ptr, s0 / 256, T, d->stream);
+    if (e != hipSuccess) {
+        stage.release();
+        PT_HIP(e);
+    }
+    const int w = DeviceWait(d);
+    stage.release();
+    return w;
+}
+
+int ptWriteBasicRendererState(pt_device* d, pt_basic_renderer* r, const pt_pixel_state* in)
+{
+    return ptWriteBasicRendererStreamState(d, r, 0, in);
+}
+
+// A stream's own accumulator (width x height rgba32f; one stream: the sample
+// buffer itself), for saving and restoring a multi-stream render.
+static float4* StreamAccumulator(pt_basic_renderer* r, uint32_t stream)
+{
+    return r->streams == 1 ? r->buffer->accum : r->accx.ptr + (size_t)stream * r->buffer->width * r->buffer->height;
+}
+
+int ptReadBasicRendererStreamAccumulator(pt_device* d, pt_basic_renderer* r, uint32_t stream, float* rgba)
+{
+    if (!d || !r || !r->buffer || !rgba) { SetError("null argument"); return -1; }
+    if (stream >= r->streams) { SetError("stream %u >= the renderer's %u streams", stream, r->streams); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    PT_HIP(hipMemcpyAsync(rgba, StreamAccumulator(r, stream), (size_t)r->buffer->width * r->buffer->height * 16,
+                          hipMemcpyDeviceToHost, d->stream));
+    PT_WAIT(d);
+    return 0;
+}
+
+int ptWriteBasicRendererStreamAccumulator(pt_device* d, pt_basic_renderer* r, uint32_t stream, const float* rgba)
+{
+    if (!d || !r || !r->buffer || !rgba) { SetError("null argument"); return -1; }
+    if (stream >= r->streams) { SetError("stream %u >= the renderer's %u streams", stream, r->streams); return -1; }
+    PT_HIP(hipSetDevice(d->id));
+    PT_HIP(hipMemcpyAsync(StreamAccumulator(r, stream), rgba, (size_t)r->buffer->width * r->buffer->height * 16,
+                          hipMemcpyHostToDevice, d->stream));
+    PT_WAIT(d);
+    return 0;
+}
+
+static_assert(PT_SHADE_DIFFUSE == PT_MATS_DIFFUSE && PT_SHADE_METAL == PT_MATS_METAL &&
+              PT_SHADE_TRANSLUCENT == PT_MATS_TRANSLUCENT && PT_SHADE_SCATTER == PT_MATS_SCATTER &&
+              PT_SHADE_OPENPBR == PT_MATS_OPENPBR && PT_SHADE_PRIMS == PT_MATS_PRIMS && PT_SHADE_SKY == PT_MATS_SKY &&
+              PT_SHADE_TEXWRAP == PT_MATS_TEXWRAP, "pt_api.h shade mask bits");
+
+int ptGetBasicRendererShadeInfo(pt_basic_renderer* r, pt_shade_info* info)
+{
+    if (!r || !info) { SetError("null argument"); return -1; }
+    if (!r->scene || !r->scene->valid) { SetError("renderer: scene has no valid packs (call ptUpdateScene)"); return -1; }
+    info->scene_mask = ShadeMats(r);
+    info->kernel_mask = pt_shade_mats(ShadeMats(r));
+    info->completion_queue = ShadeCompact(r) ? 1u : 0u;
+    info->grey_records = r->grey ? 1u : 0u;
+    return 0;
 }
 
 pt_preview* ptCreatePreviewRenderContext(pt_device* d, pt_scene* s)
@@ -1616,11 +1810,18 @@ pt_comm* ptCommCreate(pt_device* d, int nranks, int rank, const uint8_t id[128])
     c->dev = d;
     c->nranks = nranks;
     c->rank = rank;
-    if (hipMalloc(&c->flag, sizeof(int)) != hipSuccess) { SetError("comm flag allocation failed"); delete c; return nullptr; }
+    if (hipMalloc(&c->flag, sizeof(int)) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&c->host_flag), sizeof(int), hipHostMallocDefault) != hipSuccess) {
+        SetError("comm flag allocation failed");
+        if (c->flag) (void)hipFree(c->flag);
+        delete c;
+        return nullptr;
+    }
     ncclResult_t e = ncclCommInitRank(&c->comm, nranks, u, rank);
     if (e != ncclSuccess) {
         SetError("ncclCommInitRank: %s", ncclGetErrorString(e));
         (void)hipFree(c->flag);
+        (void)hipHostFree(c->host_flag);
         delete c;
         return nullptr;
     }
@@ -1631,11 +1832,19 @@ pt_comm* ptCommCreate(pt_device* d, int nranks, int rank, const uint8_t id[128])
 void ptCommDestroy(pt_comm* c)
 {
     if (!c) return;
-    pt_device* d = c->dev;
-    auto& v = d->comms;
-    v.erase(std::remove(v.begin(), v.end(), c), v.end());
+    if (pt_device* d = c->dev) {
+        (void)hipSetDevice(d->id);
+        auto& v = d->comms;
+        v.erase(std::remove(v.begin(), v.end(), c), v.end());
+        // A CommAgree readback left queued by a wait that failed (which
+        // aborted the communicator) lands before the pinned word is freed:
+        // the abort stops RCCL's kernels, and after an abort a wait gives up
+        // within 10 s.
+        if (c->aborted) (void)DeviceWait(d);
+    }
     if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->flag) (void)hipFree(c->flag);
+    if (c->host_flag) (void)hipHostFree(c->host_flag);
     delete c;
 }
 
@@ -1651,6 +1860,7 @@ namespace {
 int CommUsable(pt_device* d, pt_comm* c)
 {
     if (!d || !c) { SetError("null argument"); return -1; }
+    if (!c->dev) { SetError("communicator's device was destroyed"); return -1; }
     if (c->aborted || !c->comm) {
         SetError("communicator aborted after an earlier failure (rank %d of %d)", c->rank, c->nranks);
         return PT_ERROR_COMM_ABORTED;
@@ -1681,12 +1891,17 @@ int CommEnqueued(pt_device* d, pt_comm* c, ncclResult_t e, const char* what)
 int CommAgree(pt_device* d, pt_comm* c, int bad, const char* what)
 {
     if (c->nranks == 1) return bad ? -1 : 0;
-    int h = bad ? 1 : 0;
-    PT_HIP(hipMemcpyAsync(c->flag, &h, sizeof(int), hipMemcpyHostToDevice, d->stream));
+    // Pinned host word both ways: the copies are truly asynchronous, so a
+    // hung peer is seen by DeviceWait's polling (a pageable copy would block
+    // inside hipMemcpyAsync), and a readback still queued when the wait gives
+    // up writes into memory that lives until ptCommDestroy.
+    *c->host_flag = bad ? 1 : 0;
+    PT_HIP(hipMemcpyAsync(c->flag, c->host_flag, sizeof(int), hipMemcpyHostToDevice, d->stream));
     ncclResult_t e = ncclAllReduce(c->flag, c->flag, 1, ncclInt32, ncclMax, c->comm, d->stream);
     if (int r = CommEnqueued(d, c, e, what)) return r;
-    PT_HIP(hipMemcpyAsync(&h, c->flag, sizeof(int), hipMemcpyDeviceToHost, d->stream));
+    PT_HIP(hipMemcpyAsync(c->host_flag, c->flag, sizeof(int), hipMemcpyDeviceToHost, d->stream));
     PT_WAIT(d);
+    const int h = *c->host_flag;
     if (h && !bad) {
         SetError("%s: the arguments failed their check on another rank; nothing was exchanged", what);
         return -1;

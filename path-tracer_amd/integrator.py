@@ -256,8 +256,11 @@ class BasicRenderer:
         return int(N.hip_lib().ptBasicRendererSlotCount(self._h))
 
     def merge_streams(self):
-        """Add streams 1.. into the sample buffer (stream order) and clear
-        them (ptMergeBasicRendererStreams); a no-op for one stream."""
+        """The sample buffer's owned pixels := the sum of every stream's
+        accumulator, stream 0 included, in stream order
+        ((A0 + A1) + A2 ...; ptMergeBasicRendererStreams).  The streams are
+        not cleared and keep accumulating, so a later merge writes the new
+        totals (not deltas).  A no-op for one stream."""
         _check(N.hip_lib().ptMergeBasicRendererStreams(self.device.handle, self._h), "ptMergeBasicRendererStreams")
 
     def set_fused_rounds(self, mode: int):
@@ -334,6 +337,42 @@ class BasicRenderer:
         _check(N.hip_lib().ptReadBasicRendererStreamState(self.device.handle, self._h, int(stream), out.ctypes.data),
                "ptReadBasicRendererStreamState")
         return out.reshape(sb.height, sb.width)
+
+    def write_state(self, state: np.ndarray, stream: int = 0):
+        """Resume: restore every owned pixel's live path of one stream from a
+        saved read_state() (ptWriteBasicRendererStreamState): the next ray and
+        the path record; the trace record is not needed (the next run traces
+        first).  With the sample buffer (SampleBuffer.write) and FrameIndex
+        restored too, later runs equal the uninterrupted render bit for bit."""
+        sb = self.sample_buffer
+        a = np.ascontiguousarray(state, dtype=N.PIXEL_STATE_DTYPE).reshape(-1)
+        if a.size != sb.width * sb.height:
+            raise ValueError(f"state has {a.size} pixels, the sample buffer {sb.width * sb.height}")
+        _check(N.hip_lib().ptWriteBasicRendererStreamState(self.device.handle, self._h, int(stream), a.ctypes.data),
+               "ptWriteBasicRendererStreamState")
+
+    def read_accumulator(self, stream: int = 0) -> np.ndarray:
+        """One path stream's own accumulator (H, W, 4) (the sample buffer for one stream)."""
+        sb = self.sample_buffer
+        out = np.zeros((sb.height, sb.width, 4), dtype=np.float32)
+        _check(N.hip_lib().ptReadBasicRendererStreamAccumulator(self.device.handle, self._h, int(stream), N.fptr(out)),
+               "ptReadBasicRendererStreamAccumulator")
+        return out
+
+    def write_accumulator(self, rgba: np.ndarray, stream: int = 0):
+        """Restore one path stream's own accumulator (resume of a multi-stream render)."""
+        sb = self.sample_buffer
+        a = np.ascontiguousarray(rgba, dtype=np.float32).reshape(sb.height, sb.width, 4)
+        _check(N.hip_lib().ptWriteBasicRendererStreamAccumulator(self.device.handle, self._h, int(stream), N.fptr(a)),
+               "ptWriteBasicRendererStreamAccumulator")
+
+    def shade_info(self) -> dict:
+        """The shade variant this renderer runs (diagnostic, ptGetBasicRendererShadeInfo):
+        scene / kernel PT_SHADE_* masks, completion queue, grey path records."""
+        info = N.pt_shade_info()
+        _check(N.hip_lib().ptGetBasicRendererShadeInfo(self._h, C.byref(info)), "ptGetBasicRendererShadeInfo")
+        return {"scene_mask": int(info.scene_mask), "kernel_mask": int(info.kernel_mask),
+                "completion_queue": bool(info.completion_queue), "grey_records": bool(info.grey_records)}
 
     def close(self):
         if self._h:
