@@ -91,10 +91,13 @@ def cpu_model():
     return None
 
 
-def cpu_baseline(pt, scene, width, height, config, max_seconds=12.0, max_rounds=200):
+def cpu_baseline(pt, scene, width, height, config, settle_rounds=34, min_rounds=32, max_seconds=30.0):
     """Time the CPU oracle (scalar C++ restatement, std::thread over host
-    cores) on the same scene and frame.  Bounded: Reset + Run(2) warm-up, then
-    single rounds until max_seconds of timed work or max_rounds.
+    cores) on the same scene and frame.  Bounded: Reset + Run(2) and
+    `settle_rounds` untimed rounds (the path population past its first,
+    shortest rounds: the per-round cost is then stationary, as in
+    tools/cpu_scaling.py), then at least `min_rounds` timed single rounds,
+    more while under max_seconds.
 
     Threads: every CPU this process may run on (its affinity mask), capped by
     OMP_NUM_THREADS when set -- on the GPU box that is the job's CPU share
@@ -112,10 +115,12 @@ def cpu_baseline(pt, scene, width, height, config, max_seconds=12.0, max_rounds=
     o.RenderFlags = 3
     o.reset()
     o.run(2)
+    for _ in range(settle_rounds):
+        o.run(1)
     r0, s0 = o.counters()
     t0 = time.perf_counter()
     rounds = 0
-    while rounds < max_rounds:
+    while rounds < min_rounds or time.perf_counter() - t0 < max_seconds / 2:
         o.run(1)
         rounds += 1
         if time.perf_counter() - t0 > max_seconds:
@@ -135,9 +140,8 @@ def cpu_baseline(pt, scene, width, height, config, max_seconds=12.0, max_rounds=
         "omp_num_threads": omp or None,
         "cpu_model": cpu_model(),
         "kind": "port",
-        "sample": f"C{config} {width}x{height}, {rounds} rounds after Reset+Run(2) warm-up "
-                  f"({(r1 - r0)} rays, {(s1 - s0)} samples, {dt:.1f} s; the rate is stationary after the first "
-                  f"rounds, SURVEY.md §8(d))",
+        "sample": f"C{config} {width}x{height}, {rounds} consecutive rounds after Reset + Run(2) + "
+                  f"{settle_rounds} settle rounds ({(r1 - r0)} rays, {(s1 - s0)} samples, {dt:.1f} s timed)",
         "msamples_per_s": round((s1 - s0) / dt / 1e6, 4),
     }
 
@@ -423,6 +427,35 @@ def main():
     prof = profile_for(pkey) or {}
     kprof = prof.get("kernels", {}).get(dom, {})
     traffic = kprof.get("hbm_bytes")
+    # The roofline that binds the dominant kernel: its
+    # committed PMC's VALU issue fraction x active lanes / 64 (the fraction of
+    # the chip's lane-issue capacity doing useful work) against the HBM
+    # fraction its measured traffic reaches; the larger names the binding
+    # resource.  `frac` stays the algorithmic-bytes HBM fraction, comparable
+    # across rounds.
+    dissue = (prof.get("issue") or {}).get(dom) or {}
+    issue_frac = (round(dissue["valu_issue_frac"] * dissue["valu_active_lanes"] / 64.0, 4)
+                  if "valu_issue_frac" in dissue and "valu_active_lanes" in dissue else None)
+    traffic_frac = (round(traffic / (kernels[dom]["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+                    if traffic is not None else None)
+    if issue_frac is None or traffic_frac is None:
+        binding = None
+    elif dissue.get("valu_issue_frac", 0) > traffic_frac:
+        binding = "valu_issue"
+    else:
+        binding = "hbm"
+    # Which image property the N-GPU frame keeps (VERDICT r04 #7 / ADVICE r04):
+    # band partitions with one path stream are the one-GPU frame bit for bit;
+    # sample shards and band path streams add independent RNG streams
+    # (FrameIndex offsets), the same estimator with the same sample count.
+    if world == 1 and streams == 1:
+        identity = "bit-identical to the reference integrator's frame (oracle-checked at every config)"
+    elif shard == "bands" and streams == 1:
+        identity = "bit-identical to the 1-GPU frame (disjoint bands, same seeds)"
+    else:
+        identity = (f"same estimator as the 1-GPU frame, not bit-identical: "
+                    + (f"{streams} path streams per pixel seeded FrameIndex + (k << 24)" if shard == "bands"
+                       else "each rank's RNG stream starts at FrameIndex + (rank << 24)"))
     xname = "RCCL" if exchange == "rccl" else "gloo (host-memory fallback)"
     metric = ("Mrays/s + Msamples/s, Viking Room 1920x1080 1024spp, 1/2/4/8 GPUs" if args.config == 3 and spp == 1024
               else f"Mrays/s + Msamples/s, C{args.config} {info.width}x{info.height} {spp}spp")
@@ -458,6 +491,7 @@ def main():
             "slots_per_launch_rank0": slots_owned,
             "frame_target_samples_rank0": target,
             "mesh_faces": info.mesh_face_count,
+            "image_identity": identity,
             "parallelism": (f"pixel-bands x{world}" + (f" + {xname} band gather to rank 0" if world > 1 else "")
                             if shard == "bands" else
                             f"sample-shards x{world}" + (f" + {xname} reduce of radiance + sample counts to rank 0"
@@ -489,6 +523,13 @@ def main():
             "launches_timed": {**{k: v[0] for k, v in kstats.items()}, "every_nth_round": args.profile_period},
             "rounds_timed": {k: v[2] for k, v in kstats.items()},
             "path_gbps_220B_per_ray": round(PATH_BYTES_PER_RAY * rays / dt / 1e9, 2),
+            # BASELINE.md's whole-path definition: 220 B per ray over the frame time.
+            "path_frac": round(PATH_BYTES_PER_RAY * rays / dt / 1e9 / HBM_PEAK_GBPS, 5),
+            # The dominant kernel's measured HBM traffic (PMC) over its launch time.
+            "traffic_frac": traffic_frac,
+            # valu_issue_frac x active lanes / 64 from the same committed PMC.
+            "issue_frac": issue_frac,
+            "binding": binding,
         },
         # What bounds the dominant kernel instead of HBM (PMC of this config's
         # committed profile): fraction of the chip's VALU issue slots used and

@@ -272,7 +272,7 @@ int                ptReadBasicRendererStreamState(pt_device* device, pt_basic_re
  * a miss until then.  With the accumulator (ptWriteSampleBuffer) and
  * FrameIndex restored too, the following Runs equal the uninterrupted
  * render's bit for bit.  Fails, writing nothing, if a sample is non-zero (a
- * live path's is 0 between rounds), a lambda0 lies outside [0, 1) or an
+ * live path's is 0 between rounds), a lambda0 lies outside [0, 1] or an
  * active entry is neither 0xFFFF nor a shape of the scene.  Synchronises. */
 int                ptWriteBasicRendererState(pt_device* device, pt_basic_renderer* renderer, const pt_pixel_state* in);
 int                ptWriteBasicRendererStreamState(pt_device* device, pt_basic_renderer* renderer, uint32_t stream,

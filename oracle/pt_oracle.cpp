@@ -1457,6 +1457,8 @@ oracle_renderer* oracle_create(const pt_scene_packs* packs, uint32_t width, uint
 void oracle_destroy(oracle_renderer* r) { delete r; }
 pt_basic_renderer_params* oracle_params(oracle_renderer* r) { return &r->Params; }
 void oracle_set_openpbr(oracle_renderer* r, int enable) { r->OpenPBR = enable != 0; }
+// Worker threads of the following rounds (1..64; the CPU baseline's scaling runs).
+void oracle_set_threads(oracle_renderer* r, int threads) { r->Threads = std::max(1, std::min(threads, 64)); }
 void oracle_set_slab_division(int ieee) { SlabDivisionIEEE.store(ieee != 0); }
 int oracle_slab_division(void) { return SlabDivisionIEEE.load(); }
 float oracle_intersect_bounding_box(const float origin[3], const float velocity[3], float reach, const float mn[3],

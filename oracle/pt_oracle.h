@@ -30,6 +30,7 @@ void oracle_destroy(oracle_renderer* r);
 pt_basic_renderer_params* oracle_params(oracle_renderer* r);
 /* OpenPBR shading on/off (ptSetBasicRendererOpenPBR); off by default. */
 void oracle_set_openpbr(oracle_renderer* r, int enable);
+void oracle_set_threads(oracle_renderer* r, int threads);
 /* Slab-test division convention for every later Trace() in this process:
  * 1 = correctly rounded IEEE (Min-O) / V (default: the HIP kernels' and
  * SURVEY.md §7/§8(c)'s convention), 0 = reciprocal multiply

@@ -1364,7 +1364,7 @@ int ptReadBasicRendererState(pt_device* d, pt_basic_renderer* r, pt_pixel_state*
 // reports a miss.  Sample must be 0: a live path's Sample is 0 between rounds
 // (StorePathVertex, kernels.hip).  Checked before anything is written: every
 // active-stack entry is 0xFFFF or a shape of the scene, lambda0 lies in
-// [0, 1).
+// [0, 1].
 int ptWriteBasicRendererStreamState(pt_device* d, pt_basic_renderer* r, uint32_t stream, const pt_pixel_state* in)
 {
     if (!d || !in) { SetError("null argument"); return -1; }
@@ -1389,8 +1389,8 @@ int ptWriteBasicRendererStreamState(pt_device* d, pt_basic_renderer* r, uint32_t
             SetError("pixel (%u, %u): a live path's sample is 0 between rounds", x, y);
             return -1;
         }
-        if (!(S.lambda0 >= 0.0f && S.lambda0 < 1.0f)) {
-            SetError("pixel (%u, %u): lambda0 %g outside [0, 1)", x, y, (double)S.lambda0);
+        if (!(S.lambda0 >= 0.0f && S.lambda0 <= 1.0f)) {   // R01() of basic_scatter.glsl:40 (can round to 1)
+            SetError("pixel (%u, %u): lambda0 %g outside [0, 1]", x, y, (double)S.lambda0);
             return -1;
         }
         const uint32_t e[4] = {S.active01 & 0xFFFFu, S.active01 >> 16, S.active23 & 0xFFFFu, S.active23 >> 16};

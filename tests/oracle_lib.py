@@ -34,6 +34,7 @@ def lib():
         L.oracle_params.restype = vp
         L.oracle_params.argtypes = [vp]
         L.oracle_set_openpbr.argtypes = [vp, C.c_int]
+        L.oracle_set_threads.argtypes = [vp, C.c_int]
         L.oracle_set_slab_division.argtypes = [C.c_int]
         L.oracle_slab_division.restype = C.c_int
         L.oracle_intersect_bounding_box.restype = f32
@@ -115,6 +116,10 @@ class OracleRenderer:
     def set_openpbr(self, enable):
         """OpenPBR shading on/off (ptSetBasicRendererOpenPBR's counterpart)."""
         lib().oracle_set_openpbr(self._h, int(bool(enable)))
+
+    def set_threads(self, threads):
+        """Worker threads of the following rounds (CPU baseline scaling)."""
+        lib().oracle_set_threads(self._h, int(threads))
 
     def reset(self):
         lib().oracle_reset(self._h)

@@ -31,6 +31,18 @@ def test_gpus2_self_launches_two_ranks():
     assert d["max_over_ranks"] == 2.0 and d["reduce_ok"]
 
 
+def test_gpus8_self_launches_eight_ranks():
+    """The driver's N = 8 launch: eight self-launched gloo
+    ranks, one line from rank 0 with n_gpus 8 and the max over all ranks."""
+    p = run_bench(["--gpus", "8", "--launch-check"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["world_size"] == 8 and d["config"]["comm_ranks"] == 8
+    assert d["max_over_ranks"] == 8.0 and d["reduce_ok"]
+
+
 def test_world_size_must_match_gpus():
     p = run_bench(["--gpus", "4", "--launch-check"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert p.returncode == 2 and "WORLD_SIZE=2 but --gpus 4" in p.stderr

@@ -150,7 +150,7 @@ def test_resume_band_streams(pt, dev):
 
 def test_state_write_rejects_invalid_paths(pt, dev):
     """Nothing is written when a path is not one a renderer can hold between
-    rounds: a non-zero Sample, lambda0 outside [0, 1), an active shape index
+    rounds: a non-zero Sample, lambda0 outside [0, 1], an active shape index
     beyond the scene."""
     s = scene_for(pt, 2)
     W, H = 48, 32
@@ -163,7 +163,7 @@ def test_state_write_rejects_invalid_paths(pt, dev):
     shapes = len(s.arrays()["shapes"])
     bad_cases = []
     x = good.copy(); x["sample"][3, 5, 1] = 0.5; bad_cases.append((x, "sample"))
-    x = good.copy(); x["lambda0"][0, 0] = 1.0; bad_cases.append((x, "lambda0"))
+    x = good.copy(); x["lambda0"][0, 0] = 1.5; bad_cases.append((x, "lambda0"))
     x = good.copy(); x["active01"][2, 2] = 0xFFFF0000 | shapes; bad_cases.append((x, "active shape"))
     for st, what in bad_cases:
         with pytest.raises(pt.PathTracerError, match=what):
