@@ -180,6 +180,10 @@ int       ptSetSceneHitRecordForm(pt_scene* scene, uint32_t form);
  * BLAS depth, each capped at the reference's Stack[32]); the extend kernel keeps
  * 20 in LDS and spills the rest to a per-ray global buffer. */
 int       ptSceneStackNeeded(pt_scene* scene, uint32_t* entries);
+/* BLAS child pairs the extend kernel keeps in LDS for the uploaded scene
+ * (the top levels of its BLASes, laid out first in the device node array;
+ * 0 = no cache: scenes whose stack entries need 32 bits, or no mesh). */
+int       ptSceneNodeCache(pt_scene* scene, uint32_t* pairs);
 
 pt_sample_buffer* ptCreateSampleBuffer(pt_device* device, uint32_t width, uint32_t height);
 void              ptDestroySampleBuffer(pt_device* device, pt_sample_buffer* buffer);

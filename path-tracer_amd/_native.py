@@ -275,6 +275,7 @@ HIP_API = {
     "ptExtendStepCounts": (_i32, [_vp, _vp, _vp]),
     "ptSetProfilingPeriod": (_i32, [_vp, C.c_uint32]),
     "ptSceneStackNeeded": (_i32, [_vp, C.POINTER(C.c_uint32)]),
+    "ptSceneNodeCache": (_i32, [_vp, C.POINTER(C.c_uint32)]),
     "ptSetProfiling": (_i32, [_vp, _i32]),
     "ptGetKernelStats": (_i32, [_vp, _i32, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
     "ptGetKernelRounds": (_i32, [_vp, _i32, C.POINTER(C.c_uint64)]),
@@ -292,8 +293,14 @@ _scene_lib = None
 _hip_lib = None
 
 
-def _bind(lib, table):
+def _bind(lib, table, required=True):
+    """Set every entry point's ctypes signature.  required=False (a
+    PT_HIP_LIB experiment build of an older tree, A/B timing only) skips the
+    entry points that build lacks; calling one then raises AttributeError.
+    The in-tree library must export all of them (tests/test_abi.py)."""
     for name, (res, args) in table.items():
+        if not required and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -324,7 +331,7 @@ def hip_lib():
         if not path.exists():
             raise NativeLibraryMissing(f"{path} not built (run __graft_entry__.build())")
         lib = C.CDLL(str(path))
-        _hip_lib = _bind(lib, HIP_API)
+        _hip_lib = _bind(lib, HIP_API, required="PT_HIP_LIB" not in os.environ)
     return _hip_lib
 
 

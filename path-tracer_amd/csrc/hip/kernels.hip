@@ -1178,7 +1178,7 @@ PT_DEV void ExtendRay(const dscene& S, const Src& src, tstack<SPILL, CAP, E>& st
 // One tile of extend: thread i traces the ray at position tile*256 + i.
 template <class Src, bool SPILL, int CAP, class E>
 PT_DEV void ExtendTile(const dscene& S, const Src& src, uint32_t n, uint32_t* spill, uint32_t spill_stride, E* smem,
-                       uint32_t tile, bool timed)
+                       uint32_t tile, bool timed, const float4* nc = nullptr, uint32_t ncn = 0)
 {
     uint64_t t0 = timed ? __builtin_amdgcn_s_memtime() : 0;
     uint32_t slot = tile * 256 + threadIdx.x;
@@ -1187,6 +1187,8 @@ PT_DEV void ExtendTile(const dscene& S, const Src& src, uint32_t n, uint32_t* sp
     st.lds = &smem[threadIdx.x];
     st.spill = spill + slot;
     st.stride = spill_stride;
+    st.nc = nc;
+    st.ncn = ncn;
     ExtendRay<SPILL, CAP, E>(S, src, st, slot);
     if constexpr (kRendererSource<Src>) {
         if (timed && (threadIdx.x & 63u) == 0)
@@ -1194,11 +1196,24 @@ PT_DEV void ExtendTile(const dscene& S, const Src& src, uint32_t n, uint32_t* sp
     }
 }
 
-template <class Src, bool SPILL, int MINW, int CAP, class E = uint32_t>
+// The LDS node cache's fill: nodes [0, S.node_cache) of the scene (the top
+// child pairs, NodeCacheLayout), 16 B per thread and load, then a barrier
+// before any lane traverses.
+PT_DEV uint32_t NodeCacheFill(const dscene& S, float4* nc)
+{
+    const uint32_t nodes = min(S.node_cache, 2u * PT_NODE_CACHE_PAIRS);
+    for (uint32_t i = threadIdx.x; i < 2 * nodes; i += 256) nc[i] = S.mesh_nodes[i];
+    __syncthreads();
+    return nodes;
+}
+
+template <class Src, bool SPILL, int MINW, int CAP, class E = uint32_t, bool NC = false>
 __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, uint32_t n, uint32_t* spill,
                                                                   uint32_t spill_stride)
 {
     __shared__ E smem[CAP * 256];
+    __shared__ float4 ncache[NC ? 4 * PT_NODE_CACHE_PAIRS : 1];
+    const uint32_t ncn = NC ? NodeCacheFill(S, ncache) : 0u;
     // Tile order: the slot renderer dispatches the tiles whose waves took
     // longest in the previous round first (tile_order_kernel), so the
     // kernel's tail holds short blocks; each wave records its own time.
@@ -1210,7 +1225,7 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
             timed = true;
         }
     }
-    ExtendTile<Src, SPILL, CAP, E>(S, src, n, spill, spill_stride, smem, tile, timed);
+    ExtendTile<Src, SPILL, CAP, E>(S, src, n, spill, spill_stride, smem, tile, timed, ncache, ncn);
 }
 
 // Longest-first dispatch order for the next extend: tiles by their slowest
@@ -1784,6 +1799,15 @@ template <class Src, class E>
 static void LaunchExtendE(const ptd::dscene& S, const Src& src, uint32_t n, uint32_t blocks, uint32_t* spill,
                           hipStream_t st)
 {
+    // The LDS node cache rides beside the u16 stack only (with the u32
+    // stack's 20 KB it would cost occupancy).
+    if constexpr (sizeof(E) == 2) {
+        if (!spill && S.node_cache) {
+            hipLaunchKernelGGL((ptd::extend_kernel<Src, false, PT_EXTEND_MINW, PT_EXTEND_CAP, E, true>), dim3(blocks),
+                               dim3(256), 0, st, S, src, n, spill, n);
+            return;
+        }
+    }
     if (spill)
         hipLaunchKernelGGL((ptd::extend_kernel<Src, true, PT_EXTEND_MINW, PT_EXTEND_CAP, E>), dim3(blocks), dim3(256),
                            0, st, S, src, n, spill, n);

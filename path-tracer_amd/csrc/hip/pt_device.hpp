@@ -48,7 +48,17 @@ struct dscene {
     uint32_t vidx21;               // every vertex index fits 21 bits: hit records carry a face's vertex indices
     float vmf_inv_kappa, vmf_exp_m2k, vmf_norm;   // VmfConstants(g.SkyboxConcentration), set on upload
     float sky_flat;                // SampleParametricSpectrum((0, 0, 100), L) for any finite L (SkyFlat)
+    uint32_t node_cache;           // BLAS nodes [0, node_cache) are the top child pairs the extend kernel
+                                   // keeps in LDS (NodeCacheLayout, runtime.hip); 0: no cache
 };
+
+// LDS node cache of the extend kernel: this many BLAS child pairs (64 B
+// each), the top levels of the scene's BLASes, are loaded into LDS once per
+// block (10 KB beside the 10 KB u16 stack: 8 blocks per CU, the occupancy the
+// kernel's VGPRs allow).
+#ifndef PT_NODE_CACHE_PAIRS
+#define PT_NODE_CACHE_PAIRS 160
+#endif
 
 struct ray { pt3 Origin; pt3 Velocity; float Duration; };
 struct medium { uint32_t Priority; pt4 IOR, AbsorptionRate, ScatteringRate; float ScatteringAnisotropy; };

@@ -120,6 +120,9 @@ struct pt_scene {
     uint32_t mats = PT_MATS_ALL | PT_MATS_SCENE; // SceneMaterialMask (shade specialisation)
     uint32_t stack_format = PT_STACK_FORMAT_AUTO;   // ptSetSceneStackFormat (applied at the next update)
     uint32_t hit_record = PT_HIT_RECORD_AUTO;       // ptSetSceneHitRecordForm (applied at the next update)
+    uint32_t cached_pairs = 0;   // BLAS child pairs at the front of the device node array (NodeCacheLayout)
+    bool blas_packable = false;  // BlasWordsPackable / BlasWords16FirstBits of the device node layout
+    uint32_t blas16_bits = 0;
     bool valid = false;
 };
 
@@ -630,6 +633,70 @@ static bool MaterialReadsUV(const pt_scene_packs* p, uint32_t m)
     }
 }
 
+// LDS node cache layout (the extend kernel's NodeCacheFill, pt_device.hpp
+// PT_NODE_CACHE_PAIRS): the BLAS child pairs in breadth-first order from every
+// mesh root -- the top levels, which most node fetches of a frame read (C3:
+// the first 6 levels, 120 pairs, take 59 % of the internal-node visits) --
+// the first PT_NODE_CACHE_PAIRS of them moved to the front of the device node
+// array (pair j at nodes 2j, 2j+1), every other node after them in its
+// original order, child-pair and root indices remapped.  The numbering enters
+// no result: the traversal's decisions read only the nodes' bounds and face
+// ranges, so a renumbered BVH is traversed in the same order to the same
+// hits.  Returns the cached pair count, 0 (and the identity layout) when some
+// node is the first child of one pair and the second of another, which no
+// layout of adjacent pairs can hold.
+static uint32_t NodeCacheLayout(const pt_scene_packs* p, std::vector<pt_packed_mesh_node>& out,
+                                std::vector<uint32_t>& remap)
+{
+    const uint32_t n = p->mesh_node_count;
+    const pt_packed_mesh_node* in = p->mesh_nodes;
+    out.assign(in, in + n);
+    remap.resize(n);
+    for (uint32_t i = 0; i < n; i++) remap[i] = i;
+    if (n < 3) return 0;
+    std::vector<uint8_t> role(n, 0);   // 1: first node of a child pair, 2: second
+    for (uint32_t i = 0; i < n; i++) {
+        if (in[i].FaceEndIndex > 0) continue;
+        const uint32_t c = in[i].FaceBeginOrNodeIndex;
+        if (c + 1 >= n) return 0;
+        role[c] |= 1;
+        role[c + 1] |= 2;
+    }
+    for (uint32_t i = 0; i < n; i++)
+        if (role[i] == 3) return 0;
+    std::vector<uint32_t> cached, queue;
+    std::vector<uint8_t> seen(n, 0);
+    for (uint32_t k = 0; k < p->shape_count; k++) {
+        if (p->shapes[k].Type != PT_SHAPE_TYPE_MESH_INSTANCE) continue;
+        const uint32_t r = p->shapes[k].MeshRootNodeIndex;
+        if (r < n && in[r].FaceEndIndex == 0) queue.push_back(in[r].FaceBeginOrNodeIndex);
+    }
+    for (size_t h = 0; h < queue.size() && cached.size() < PT_NODE_CACHE_PAIRS; h++) {
+        const uint32_t c = queue[h];
+        if (seen[c]) continue;
+        seen[c] = 1;
+        cached.push_back(c);
+        for (uint32_t m = c; m <= c + 1; m++)
+            if (in[m].FaceEndIndex == 0) queue.push_back(in[m].FaceBeginOrNodeIndex);
+    }
+    if (cached.empty()) return 0;
+    std::vector<uint8_t> moved(n, 0);
+    for (uint32_t j = 0; j < cached.size(); j++) {
+        remap[cached[j]] = 2 * j;
+        remap[cached[j] + 1] = 2 * j + 1;
+        moved[cached[j]] = moved[cached[j] + 1] = 1;
+    }
+    uint32_t next = 2 * (uint32_t)cached.size();
+    for (uint32_t i = 0; i < n; i++)
+        if (!moved[i]) remap[i] = next++;
+    for (uint32_t i = 0; i < n; i++) {
+        pt_packed_mesh_node N = in[i];
+        if (N.FaceEndIndex == 0) N.FaceBeginOrNodeIndex = remap[N.FaceBeginOrNodeIndex];
+        out[remap[i]] = N;
+    }
+    return (uint32_t)cached.size();
+}
+
 // Material types reachable by a hit (every shape's material), whether any
 // medium can scatter, whether any shape is not a mesh instance and whether sky
 // light sampling is on: selects the shade kernel instantiation (kernels.hip
@@ -703,12 +770,22 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     }
     if (first || (dirty & PT_SCENE_DIRTY_MATERIALS)) PT_HIP(s->material.upload(p->material_data, p->material_word_count));
     if (first || (dirty & PT_SCENE_DIRTY_SHAPES)) PT_HIP(s->shape_nodes.upload(p->shape_nodes, p->shape_node_count));
-    if (first || (dirty & (PT_SCENE_DIRTY_SHAPES | PT_SCENE_DIRTY_MATERIALS))) {
+    // The device BLAS node array in the LDS node cache's layout (the shapes'
+    // root indices follow it).
+    const bool relayout = first || (dirty & (PT_SCENE_DIRTY_SHAPES | PT_SCENE_DIRTY_MATERIALS | PT_SCENE_DIRTY_MESHES));
+    std::vector<pt_packed_mesh_node> nodes;
+    std::vector<uint32_t> remap;
+    if (relayout) s->cached_pairs = NodeCacheLayout(p, nodes, remap);
+    if (relayout) {
         // The device's shape records carry, in their unused Pad0 word, whether
         // the shape's material reads texture coordinates (HitAttributesV).
         std::vector<pt_packed_shape> sh(p->shapes, p->shapes + p->shape_count);
-        for (pt_packed_shape& S : sh) S.Pad0 = MaterialReadsUV(p, S.MaterialIndex) ? ptd::PT_SHAPE_FLAG_UV : 0u;
+        for (pt_packed_shape& S : sh) {
+            S.Pad0 = MaterialReadsUV(p, S.MaterialIndex) ? ptd::PT_SHAPE_FLAG_UV : 0u;
+            if (S.Type == PT_SHAPE_TYPE_MESH_INSTANCE) S.MeshRootNodeIndex = remap[S.MeshRootNodeIndex];
+        }
         PT_HIP(s->shapes.upload(sh.data(), sh.size()));
+        PT_HIP(s->mesh_nodes.upload(nodes.data(), nodes.size()));
     }
     if (first || (dirty & PT_SCENE_DIRTY_MESHES)) {
         // Device face records carry {Position0, Edge1, Edge2} (traverse.hpp
@@ -727,7 +804,6 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
         PT_HIP(s->vertex_v.alloc(std::max<size_t>(p->mesh_vertex_count, 1)));
         PT_HIP(pt_launch_vertex_decode(reinterpret_cast<const uint2*>(s->vertices.ptr), p->mesh_vertex_count,
                                        s->vertex_attr.ptr, s->vertex_v.ptr, d->stream));
-        PT_HIP(s->mesh_nodes.upload(p->mesh_nodes, p->mesh_node_count));
     }
     if (first || (dirty & PT_SCENE_DIRTY_CAMERAS)) PT_HIP(s->cameras.upload(p->cameras, p->camera_count));
 
@@ -766,15 +842,25 @@ int ptUpdateScene(pt_device* d, pt_scene* s, const pt_scene_packs* p, uint32_t d
     // Traversal stack entries: 16-bit when every entry fits, else packed
     // 32-bit BLAS words, else node indices (ptSetSceneStackFormat can force
     // the wider forms, which larger scenes need).
-    D.blas_words = (s->stack_format != PT_STACK_FORMAT_NODE_INDEX && BlasWordsPackable(p)) ? 1u : 0u;
+    // (On the device node layout: its child-pair indices are what the
+    // stack entries hold.)
+    pt_scene_packs pd = *p;
+    if (relayout) pd.mesh_nodes = nodes.data();
+    D.blas_words = (s->stack_format != PT_STACK_FORMAT_NODE_INDEX && (relayout ? BlasWordsPackable(&pd) : s->blas_packable)) ? 1u : 0u;
     D.blas_firstbits = 0;
     D.stack16 = 0;
-    uint32_t F16 = s->stack_format == PT_STACK_FORMAT_AUTO ? BlasWords16FirstBits(p) : 0u;
+    uint32_t F16 = s->stack_format == PT_STACK_FORMAT_AUTO ? (relayout ? BlasWords16FirstBits(&pd) : s->blas16_bits) : 0u;
+    if (relayout) {
+        s->blas_packable = BlasWordsPackable(&pd);
+        s->blas16_bits = BlasWords16FirstBits(&pd);
+    }
     if (uint32_t F = F16) {   // every stack entry fits 16 bits
         D.blas_words = 2;
         D.blas_firstbits = F;
         D.stack16 = 1;
     }
+    // The LDS node cache rides with the u16 stack (kernels.hip LaunchExtendE).
+    D.node_cache = D.stack16 ? 2 * s->cached_pairs : 0u;
     s->camera_count = p->camera_count;
     s->stack_needed = need;
     s->valid = true;
@@ -1787,6 +1873,13 @@ int ptSceneStackNeeded(pt_scene* s, uint32_t* entries)
 {
     if (!s || !entries) { SetError("null argument"); return -1; }
     *entries = s->stack_needed;
+    return 0;
+}
+
+int ptSceneNodeCache(pt_scene* s, uint32_t* pairs)
+{
+    if (!s || !pairs) { SetError("null argument"); return -1; }
+    *pairs = s->valid ? s->d.node_cache / 2 : 0u;
     return 0;
 }
 

@@ -7,6 +7,11 @@
 
 namespace ptd {
 
+#define PT_LDS __attribute__((address_space(3)))
+#define PT_GLOBAL __attribute__((address_space(1)))
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+PT_DEV float4 F4(f32x4 v) { return make_float4(v.x, v.y, v.z, v.w); }
+
 // PT_STEP_JOIN: LaneStep's BLAS part as divergent compute + joined state
 // update (below); 0 = the branch-local updates.
 #ifndef PT_STEP_JOIN
@@ -28,6 +33,10 @@ struct tstack {
     E* lds;               // &smem[tid]; entry i at lds[i * 256] (E: u32, or u16 when every entry fits)
     uint32_t* spill;      // &spill[thread]; entry i (>= CAP) at spill[(i - CAP) * stride]
     uint32_t stride;
+    // LDS node cache (dscene::node_cache): BLAS nodes [0, ncn) at nc[2 * node]
+    // (a block-wide copy of the scene's first ncn nodes); ncn = 0: none.
+    const float4* nc = nullptr;
+    uint32_t ncn = 0;
     PT_DEV void put(uint32_t i, uint32_t v)
     {
         if (!SPILL || i < CAP) lds[i * 256] = (E)v;
@@ -467,8 +476,21 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP, SE>& st,
             ss.node(true);
             ss.internal();
             ss.coherence(L.na);
-            const float4* Np = S.mesh_nodes + 2 * (size_t)L.na;   // child pair: 64 contiguous bytes
-            float4 a0 = Np[0], a1 = Np[1], b0 = Np[2], b1 = Np[3];
+            // The child pair (64 contiguous bytes): from the block's LDS copy
+            // of the top pairs when cached (no texture-address work, LDS
+            // latency), else from global memory.
+            // (Explicit address spaces: the two sides must stay an LDS read
+            // and a global load; as generic pointers the compiler merges them
+            // into one flat load, which every lane issues through the
+            // texture-address path.)
+            float4 a0, a1, b0, b1;
+            if (L.na < st.ncn) {
+                const PT_LDS f32x4* Cp = (const PT_LDS f32x4*)st.nc + 2 * L.na;
+                a0 = F4(Cp[0]); a1 = F4(Cp[1]); b0 = F4(Cp[2]); b1 = F4(Cp[3]);
+            } else {
+                const PT_GLOBAL f32x4* Np = (const PT_GLOBAL f32x4*)S.mesh_nodes + 2 * (size_t)L.na;
+                a0 = F4(Np[0]); a1 = F4(Np[1]); b0 = F4(Np[2]); b1 = F4(Np[3]);
+            }
             IntersectBoxPair(L.O, L.V, L.Y, L.Time, a0, a1, b0, b1, L.exact, TA, TB);
             aw0 = __float_as_uint(a0.w), aw1 = __float_as_uint(a1.w);
             bw0 = __float_as_uint(b0.w), bw1 = __float_as_uint(b1.w);

@@ -122,6 +122,13 @@ class DeviceScene:
         _check(N.hip_lib().ptSceneStackNeeded(self._h, C.byref(v)), "ptSceneStackNeeded")
         return int(v.value)
 
+    @property
+    def node_cache_pairs(self) -> int:
+        """BLAS child pairs the extend kernel keeps in LDS (0: none; ptSceneNodeCache)."""
+        v = C.c_uint32(0)
+        _check(N.hip_lib().ptSceneNodeCache(self._h, C.byref(v)), "ptSceneNodeCache")
+        return int(v.value)
+
     def trace_rays(self, origins: np.ndarray, packed_velocities: np.ndarray, durations: np.ndarray) -> np.ndarray:
         """Bit-exact Trace() of a ray batch (scene.glsl.inc:522-611)."""
         o = np.ascontiguousarray(origins, dtype=np.float32).reshape(-1, 3)

@@ -172,3 +172,24 @@ def test_config_variants(pt, dev, config, grey):
     info = render_and_check(pt, dev, scene_for(pt, config), W=64, H=48)
     assert info["grey_records"] == grey
     assert info["kernel_mask"] != LEAN
+
+
+def test_node_cache_layout_is_result_neutral(pt, dev):
+    """The LDS node cache's device BVH layout (the top child pairs first,
+    every index remapped; runtime.hip NodeCacheLayout): on for the u16-stack
+    scenes, off when the stack needs 32-bit entries, and the same hits and
+    frames either way -- against the oracle, which traverses the packs'
+    original numbering."""
+    from test_gpu_parity import compare_hits, random_rays
+    for config in (3, 5):
+        s = scene_for(pt, config)
+        for fmt, cached in ((0, True), (1, False)):
+            ds = pt.DeviceScene(dev)
+            ds.set_stack_format(fmt)
+            ds.update(s)
+            assert (ds.node_cache_pairs > 0) == cached
+            if cached and config == 3:
+                assert ds.node_cache_pairs == 160
+            o, v, d = random_rays(s.arrays(), 20000, seed=40 + config)
+            compare_hits(ds.trace_rays(o, v, d), oracle_lib.trace_rays(s.packs(), o, v, d))
+            ds.close()

@@ -1,0 +1,13 @@
+# 8-rank flow checks of the multi-GPU partitions on one GPU
+# (every rank on device 0; RCCL refuses two ranks on one device, so the
+# exchange takes the gloo fallback), then the C3 PMC of the grey-record build
+# and the settled CPU-baseline thread scaling.
+set -e
+O=gpurun_out/r05_flow8; mkdir -p $O
+run() { name=$1; shift; timeout -k 10 400 python bench.py --gpus 8 --one-gpu-flow-check --no-cpu-baseline --no-steady "$@" > $O/$name.log 2>&1 || { tail -20 $O/$name.log; exit 1; }; grep '^{' $O/$name.log > $O/$name.json; python3 -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; print(sys.argv[2], d['n_gpus'], d['value'], c['shard'], c['streams'], c['exchange'], c['image_identity'], d['frame']['rounds_per_frame_rank0'])" $O/$name.json $name; }
+run c4_bands --config 4 --spp 16 --steps 2 --warmup 1
+run c3_bands --config 3 --shard bands --spp 32 --steps 2 --warmup 1
+run c3_samples --config 3 --spp 64 --steps 2 --warmup 1
+bash tools/r04/gpu_pmc.sh r05_flow8/pmc_c3 python3 $PWD/tools/run_rounds.py --config 3
+timeout -k 10 400 python tools/cpu_scaling.py $O/cpu_scaling.json > $O/cpu_scaling.log 2>&1
+tail -3 $O/cpu_scaling.log | cut -c1-600
