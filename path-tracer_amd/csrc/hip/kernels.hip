@@ -1196,148 +1196,6 @@ PT_DEV void ExtendTile(const dscene& S, const Src& src, uint32_t n, uint32_t* sp
     }
 }
 
-// --- extend with in-block ray compaction ------------------------------------------
-//
-// A wave runs until its longest ray is done: C3 averages 26 steps per ray but
-// 52 wave steps per wave, half its lanes idle (SIMD efficiency 0.49-0.53).
-// Here the block's four waves trace their tile's 256 rays PT_COMPACT_K steps at
-// a time; at each such point they count their live rays, and when the live
-// rays would fit in fewer waves, every live ray's traversal state (18 words)
-// moves through LDS to the block's lowest threads, so the higher waves go idle
-// (they wait at the barriers, issuing nothing) while the lower ones run full.
-// A ray's traversal stack stays in its home column (LDS), the ray only
-// changes thread; its steps, their order and its hit are unchanged, so the
-// results are the same bits.  Cost model (tools/exp_extend_model.py
-// on C3 per-ray step sequences): -25 % issued VALU per tile at K = 4.
-#ifndef PT_COMPACT_K
-#define PT_COMPACT_K 4
-#endif
-#ifndef PT_EXTEND_MINW
-#define PT_EXTEND_MINW 5
-#endif
-// Occupancy floor of the compacting extend: 8 waves per SIMD (<= 64 VGPRs),
-// the plain kernel's.
-#ifndef PT_COMPACT_MINW
-#define PT_COMPACT_MINW 8
-#endif
-// The compacting extend for the renderer's u16-stack scenes (A/B: 0 = off).
-#ifndef PT_EXTEND_COMPACT
-#define PT_EXTEND_COMPACT 0
-#endif
-constexpr uint32_t kXWords = 18;     // exchanged words per live ray
-constexpr uint32_t kXCap = 138;      // rays per exchange (LDS: 10 KB stack + 9.7 KB exchange = 8 blocks / CU)
-
-// A finished ray: its compact hit stored at its position, its ShadeOrder class
-// recorded for the block's end.
-PT_DEV void ExtendFinish(const dscene& S, const ray_source_slots& src, const lane_state& Ln, uint32_t slot,
-                         uint8_t* cls_lds, uint32_t home)
-{
-    src.store(slot, Ln, S.vidx21 != 0);
-    uint32_t cls = 0;
-    if (Ln.Shape == SHAPE_INDEX_NONE) {
-        cls = 4;
-    } else if (S.mat_classes) {
-        uint32_t T = S.material[32 * (size_t)S.shapes[Ln.Shape].MaterialIndex];
-        cls = T == PT_MATERIAL_TYPE_BASIC_DIFFUSE ? 0u
-            : T == PT_MATERIAL_TYPE_BASIC_METAL ? 1u
-            : T == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT ? 2u : 3u;
-    }
-    cls_lds[home] = (uint8_t)cls;
-}
-
-template <int CAP, class E>
-__global__ __launch_bounds__(256, PT_COMPACT_MINW) void extend_compact_kernel(dscene S, ray_source_slots src)
-{
-    __shared__ E smem[CAP * 256];
-    __shared__ uint32_t xb[kXWords * kXCap];
-    __shared__ uint8_t cls_lds[256];
-    __shared__ uint32_t wcount[2][4];
-    const uint32_t tile = src.L.order ? src.L.order[blockIdx.x] : blockIdx.x;
-    const bool timed = src.L.order != nullptr;
-    const uint64_t t0 = timed ? __builtin_amdgcn_s_memtime() : 0;
-    const uint32_t base = tile * 256, tid = threadIdx.x, w = tid >> 6;
-    uint32_t home = tid;
-    tstack<false, CAP, E> st;
-    st.lds = &smem[home];
-    st.spill = nullptr;
-    st.stride = 0;
-    lane_state Ln;
-    no_stats ns;
-    cls_lds[tid] = 0;
-    pt3 O, V;
-    float D;
-    bool active = src.load(base + home, O, V, D);
-    if (active) {
-        LaneBegin(S, Ln, O, V, D);
-        if (S.g.ShapeCount == 0) {
-            ExtendFinish(S, src, Ln, base + home, cls_lds, home);
-            active = false;
-        }
-    }
-    uint32_t parity = 0;
-    for (;;) {
-        for (uint32_t k = 0; k < PT_COMPACT_K; k++) {
-            if (__ballot(active) == 0) break;
-            if (active && LaneStep<false, CAP, ray_source_slots, no_stats, true, E>(S, Ln, st, src, base + home, ns)) {
-                ExtendFinish(S, src, Ln, base + home, cls_lds, home);
-                active = false;
-            }
-        }
-        const uint64_t am = __ballot(active);
-        if ((tid & 63u) == 0) wcount[parity][w] = (uint32_t)__popcll(am);
-        __syncthreads();
-        uint32_t total = 0, before = 0, waves = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < 4; i++) {
-            const uint32_t c = wcount[parity][i];
-            before += i < w ? c : 0u;
-            total += c;
-            waves += c != 0;
-        }
-        parity ^= 1u;
-        if (total == 0) break;
-        if ((total + 63) / 64 < waves && total <= kXCap) {
-            if (active) {
-                const uint32_t q = before + __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32),
-                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
-                const uint32_t v[kXWords] = {
-                    __float_as_uint(Ln.O.x), __float_as_uint(Ln.O.y), __float_as_uint(Ln.O.z),
-                    __float_as_uint(Ln.V.x), __float_as_uint(Ln.V.y), __float_as_uint(Ln.V.z),
-                    __float_as_uint(Ln.Time), Ln.Shape, Ln.Prim, Ln.HA, Ln.HB,
-                    __float_as_uint(Ln.C.x), __float_as_uint(Ln.C.y), __float_as_uint(Ln.C.z),
-                    Ln.na, Ln.nb, Ln.blas, Ln.dT | (Ln.dB << 8) | (home << 16)};
-#pragma unroll
-                for (uint32_t i = 0; i < kXWords; i++) xb[i * kXCap + q] = v[i];
-            }
-            __syncthreads();
-            active = tid < total;
-            if (active) {
-                uint32_t v[kXWords];
-#pragma unroll
-                for (uint32_t i = 0; i < kXWords; i++) v[i] = xb[i * kXCap + tid];
-                Ln.Time = __uint_as_float(v[6]);
-                Ln.Shape = v[7]; Ln.Prim = v[8]; Ln.HA = v[9]; Ln.HB = v[10];
-                Ln.C = v3(__uint_as_float(v[11]), __uint_as_float(v[12]), __uint_as_float(v[13]));
-                Ln.na = v[14]; Ln.nb = v[15]; Ln.blas = v[16];
-                Ln.dT = v[17] & 0xFFu;
-                Ln.dB = (v[17] >> 8) & 0xFFu;
-                home = v[17] >> 16;
-                st.lds = &smem[home];
-                // The level ray's reciprocal and slab-division flag are
-                // functions of the level ray (SetLevelRay): recomputed.
-                SetLevelRay(S, Ln, v3(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2])),
-                            v3(__uint_as_float(v[3]), __uint_as_float(v[4]), __uint_as_float(v[5])));
-            }
-            // (The next exchange's writes follow the next count barrier, after
-            // every wave's reads of this one.)
-        }
-    }
-    // Every ray is done: the ShadeOrder masks by position, as extend_kernel's.
-    __syncthreads();
-    src.outcome(base + tid, cls_lds[tid], S.mat_classes != 0);
-    if (timed && (tid & 63u) == 0) src.L.tilecost[tile * 4 + w] = (uint32_t)(__builtin_amdgcn_s_memtime() - t0);
-}
-
 // The LDS node cache's fill: nodes [0, S.node_cache) of the scene (the top
 // child pairs, NodeCacheLayout), 16 B per thread and load, then a barrier
 // before any lane traverses.
@@ -1944,13 +1802,6 @@ static void LaunchExtendE(const ptd::dscene& S, const Src& src, uint32_t n, uint
     // The LDS node cache rides beside the u16 stack only (with the u32
     // stack's 20 KB it would cost occupancy).
     if constexpr (sizeof(E) == 2) {
-        if constexpr (PT_EXTEND_COMPACT && ptd::kRendererSource<Src>) {
-            if (!spill) {
-                hipLaunchKernelGGL((ptd::extend_compact_kernel<PT_EXTEND_CAP, E>), dim3(blocks), dim3(256), 0, st, S,
-                                   src);
-                return;
-            }
-        }
         if (!spill && S.node_cache) {
             hipLaunchKernelGGL((ptd::extend_kernel<Src, false, PT_EXTEND_MINW, PT_EXTEND_CAP, E, true>), dim3(blocks),
                                dim3(256), 0, st, S, src, n, spill, n);
