@@ -119,6 +119,7 @@ def cpu_baseline(pt, scene, width, height, config, settle_rounds=34, min_rounds=
         o.run(1)
     r0, s0 = o.counters()
     t0 = time.perf_counter()
+    c0 = time.process_time()
     rounds = 0
     while rounds < min_rounds or time.perf_counter() - t0 < max_seconds / 2:
         o.run(1)
@@ -126,6 +127,7 @@ def cpu_baseline(pt, scene, width, height, config, settle_rounds=34, min_rounds=
         if time.perf_counter() - t0 > max_seconds:
             break
     dt = time.perf_counter() - t0
+    cpu_s = time.process_time() - c0
     r1, s1 = o.counters()
     o.close()
     share = "the job's CPU share (OMP_NUM_THREADS)" if omp > 0 and omp < allowed else "every affinity CPU"
@@ -143,6 +145,12 @@ def cpu_baseline(pt, scene, width, height, config, settle_rounds=34, min_rounds=
         "sample": f"C{config} {width}x{height}, {rounds} consecutive rounds after Reset + Run(2) + "
                   f"{settle_rounds} settle rounds ({(r1 - r0)} rays, {(s1 - s0)} samples, {dt:.1f} s timed)",
         "msamples_per_s": round((s1 - s0) / dt / 1e6, 4),
+        # The host is shared with the other GPUs' jobs: the wall-clock rate
+        # moves +-40 % between runs minutes apart.  CPU seconds
+        # the process's threads actually ran give the rate on `threads`
+        # dedicated cores, which moves less.
+        "cpu_seconds": round(cpu_s, 2),
+        "mrays_per_cpu_s_x_threads": round((r1 - r0) / max(cpu_s, 1e-9) * threads / 1e6, 4),
     }
 
 

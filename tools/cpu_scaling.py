@@ -53,19 +53,23 @@ def main():
         o.set_threads(t)
         r0, s0 = o.counters()
         t0 = time.perf_counter()
+        c0 = time.process_time()
         per_round = []
         for _ in range(a.rounds):
             t1 = time.perf_counter()
             o.run(1)
             per_round.append(time.perf_counter() - t1)
         dt = time.perf_counter() - t0
+        cpu_s = time.process_time() - c0
         r1, s1 = o.counters()
         per_round.sort()
         row = {"threads": t, "rounds": a.rounds, "seconds": round(dt, 3),
                "mrays_per_s": round((r1 - r0) / dt / 1e6, 4),
                "msamples_per_s": round((s1 - s0) / dt / 1e6, 4),
                "median_round_s": round(per_round[len(per_round) // 2], 4),
-               "min_round_s": round(per_round[0], 4), "max_round_s": round(per_round[-1], 4)}
+               "min_round_s": round(per_round[0], 4), "max_round_s": round(per_round[-1], 4),
+               "cpu_seconds": round(cpu_s, 2),
+               "mrays_per_cpu_s_x_threads": round((r1 - r0) / max(cpu_s, 1e-9) * t / 1e6, 4)}
         rows.append(row)
         print(json.dumps(row), flush=True)
     o.close()
