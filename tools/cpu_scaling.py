@@ -32,10 +32,13 @@ def main():
     ap.add_argument("--settle", type=int, default=34)
     ap.add_argument("--rounds", type=int, default=32)
     ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--init-gpu", action="store_true",
+                    help="create a HIP device first, as bench.py's process has when it times its cpu_baseline")
     a = ap.parse_args()
     import bench
     import oracle_lib  # test infrastructure: the CPU baseline, never the product path
     pt = bench.load_package()
+    dev = pt.Device(0) if a.init_gpu else None
     scene = pt.Scene.config(a.config)
     info = scene.info
     counts = [int(x) for x in a.threads.split(",")]
@@ -73,6 +76,8 @@ def main():
         rows.append(row)
         print(json.dumps(row), flush=True)
     o.close()
+    if dev is not None:
+        dev.close()
     base = rows[0]["mrays_per_s"] / rows[0]["threads"]
     for r in rows:
         r["efficiency_vs_1_thread"] = round(r["mrays_per_s"] / (base * r["threads"]), 3)
@@ -84,6 +89,7 @@ def main():
     last = rows[-1]
     out = {"config": f"C{a.config} {info.width}x{info.height}", "cpu_model": bench.cpu_model(), "host_cpus": host,
            "affinity_cpus": aff, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+           "hip_device_initialised": a.init_gpu,
            "method": f"one render: Reset, Run(2), {a.settle} settle rounds at {max(counts)} threads, then "
                      f"{a.rounds} timed consecutive rounds per thread count",
            "rows": rows,
