@@ -736,3 +736,38 @@ def test_whole_1024spp_frame_bit_exact(pt, dev):
     assert int(oa[..., 3].astype(np.float64).sum()) == samples
     for batch in (0, 1):
         assert np.array_equal(bits(out[batch][2]), bits(oa)), f"round batch mode {batch}"
+
+
+def test_comm_deadline_aborts_and_device_recovers(pt, dev):
+    """The wait's deadline branch with a live RCCL communicator (runtime.hip
+    DeviceWait): with a 1 ms deadline, waiting on 150 queued
+    full-size C3 rounds (~60 ms) gives up with PT_ERROR_TIMEOUT and aborts the
+    communicator (ncclCommAbort); exchanges on it then fail with
+    PT_ERROR_COMM_ABORTED; once the stream drains, waits succeed again and the
+    renderer's work is intact (its rays/samples counters keep counting)."""
+    s = pt.Scene.config(3)
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    sb = pt.SampleBuffer(dev, 1920, 1080)
+    r = pt.BasicRenderer(dev, ds, sb)
+    r.RenderFlags = 3
+    r.reset()
+    r.run(2)
+    dev.synchronize()
+    comm = pt.Comm(dev, 1, 0, pt.Comm.unique_id())
+    comm.set_timeout(1e-3)
+    for _ in range(150):
+        r.run(1)
+    with pytest.raises(pt.PathTracerError, match=r"status -3"):
+        dev.synchronize()
+    with pytest.raises(pt.PathTracerError, match=r"status -2"):
+        comm.reduce_sample_buffer(sb, 0)
+    dev.synchronize()                      # no live communicator: drains, then succeeds
+    rays, samples = r.stats()
+    assert rays == 152 * 1920 * 1080 and samples > 0
+    comm.close()
+    r.run(1)
+    dev.synchronize()
+    for x in (r, sb, ds):
+        x.close()
+    s.close()

@@ -224,3 +224,86 @@ def test_record_form_switches_with_openpbr(pt, dev, tmp_path):
     for x in (r, sb, ds):
         x.close()
     s.close()
+
+
+@pytest.mark.parametrize("seed", [0, 5, 10, 15, 19, 23])
+def test_resume_random_scenes(pt, dev, seed):
+    """Resume on the fuzz scenes (tests/fuzz_scenes.py: nested and scattering
+    glass, OpenPBR hits, textured skies, every camera, random flags and
+    roulette), the resumed renderer running its rounds as a round batch for
+    odd seeds: state and image equal the uninterrupted render and the oracle."""
+    import fuzz_scenes
+    s, st = fuzz_scenes.build(pt, seed)
+    W, H = 48, 32
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    kw = dict(flags=st["flags"], termination=st["termination"])
+    a, sba = renderer(pt, dev, ds, W, H, **kw)
+    a.reset()
+    a.run(2)
+    a.run(1)
+    saved, acc, frame = a.read_state(), sba.read(), a.FrameIndex
+    a.close()
+    sba.close()
+    b, sbb = renderer(pt, dev, ds, W, H, **kw)
+    sbb.write(acc)
+    b.FrameIndex = frame
+    b.write_state(saved)
+    if seed % 2:
+        b.set_round_batch(2)
+        b.run_rounds(3)
+    else:
+        for _ in range(3):
+            b.run(1)
+    o = oracle_lib.OracleRenderer(s.packs(), W, H)
+    o.RenderFlags = st["flags"]
+    o.PathTerminationProbability = st["termination"]
+    o.reset()
+    o.run(2)
+    for _ in range(4):
+        o.run(1)
+    dev.synchronize()
+    compare_state(b.read_state(), o.state())
+    assert np.array_equal(bits(sbb.read()), bits(o.accum()))
+    o.close()
+    for x in (b, sbb, ds):
+        x.close()
+    s.close()
+
+
+def test_resume_fused_small_frame(pt, dev):
+    """C1 at 256x256 (every tile resident at once: the fused round kernel and
+    automatic 16-round batches), saved after Run(2) + 5 rounds and resumed for
+    20 consecutive Run(1) rounds (batched), against the oracle."""
+    s = scene_for(pt, 1)
+    W, H = 256, 256
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    a, sba = renderer(pt, dev, ds, W, H)
+    a.reset()
+    a.run(2)
+    a.run_rounds(5)
+    saved, acc, frame = a.read_state(), sba.read(), a.FrameIndex
+    info = a.shade_info()
+    a.close()
+    sba.close()
+    assert info["grey_records"]
+    b, sbb = renderer(pt, dev, ds, W, H)
+    sbb.write(acc)
+    b.FrameIndex = frame
+    b.write_state(saved)
+    assert not b.shade_info()["grey_records"]       # written records are four-float ones ...
+    b.run_rounds(20)
+    assert b.shade_info()["grey_records"]           # ... and grey again after the next run
+    o = oracle_lib.OracleRenderer(s.packs(), W, H)
+    o.RenderFlags = 3
+    o.reset()
+    o.run(2)
+    for _ in range(25):
+        o.run(1)
+    dev.synchronize()
+    compare_state(b.read_state(), o.state())
+    assert np.array_equal(bits(sbb.read()), bits(o.accum()))
+    o.close()
+    for x in (b, sbb, ds):
+        x.close()
