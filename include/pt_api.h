@@ -311,7 +311,8 @@ typedef struct pt_shade_info {
     uint32_t scene_mask;        /* PT_SHADE_* of the scene as the renderer shades it */
     uint32_t kernel_mask;       /* the instantiation launched: the smallest superset built
                                    (PT_SHADE_DIFFUSE alone = the lean diffuse-mesh kernel) */
-    uint32_t completion_queue;  /* 1: completed paths restart through the block's queue */
+    uint32_t completion_queue;  /* 1: completed paths restart through the block's queue
+                                   (the separate extend / shade launches; fused rounds do not queue) */
     uint32_t grey_records;      /* 1: live paths keep one Probability float and no stack
                                    (as of the last Reset / Run / state write) */
 } pt_shade_info;

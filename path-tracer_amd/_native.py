@@ -154,7 +154,7 @@ TONE_MAPPING_CLAMP, TONE_MAPPING_REINHARD, TONE_MAPPING_HABLE, TONE_MAPPING_ACES
  PREVIEW_RENDER_MODE_SCENE_COMPLEXITY) = range(7)
 KERNEL_PREVIEW = 4
 KERNEL_ROUND = 5     # fused extend + shade (partitions that fit the GPU at once)
-KERNEL_SORT = 6      # global ray sort (scan + scatter) before extend
+KERNEL_ROUNDS = 6    # a round batch: several rounds of every tile in one launch (PT_KERNEL_ROUNDS)
 
 _vp = C.c_void_p
 _u32 = C.c_uint32
