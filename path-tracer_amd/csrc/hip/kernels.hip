@@ -548,22 +548,25 @@ PT_DEV medium ResolveMedium(const dscene& S, uint32_t ShapeIndex, pt4 Lambda)
 // translucent roughness / anisotropy (HasDirac reads the same roughness
 // value) before the light choice, the reflectances after the sampled
 // direction is known (a sky sample below the surface ends the path first).
-template <uint32_t MATS>
+template <uint32_t MATS, uint32_t CLS = 0xFFFFFFFFu>
 PT_DEV bool SampleSurfaceIntegrand(const dscene& S, rng& G, pt3 Nrm, pt3 TX, pt3 TY, const bsdf_parameters& P, pt3 Out,
                                    pt3& In, pt4& Throughput, pt4& Probability)
 {
     const uint32_t M = P.MaterialIndex;
     const uint32_t Type = MUint(S, M, 0);
-    const bool diffuse = (MATS & PT_MATS_DIFFUSE) && Type == PT_MATERIAL_TYPE_BASIC_DIFFUSE;
-    const bool metal = (MATS & PT_MATS_METAL) && Type == PT_MATERIAL_TYPE_BASIC_METAL;
-    const bool trans = (MATS & PT_MATS_TRANSLUCENT) && Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT;
-    const bool openpbr = (MATS & PT_MATS_OPENPBR) && Type == PT_MATERIAL_TYPE_OPENPBR;
+    // CLS: the BSDF types this instantiation samples (a class-pure launch
+    // compiles only its class's; the medium code still follows MATS).
+    constexpr uint32_t B = MATS & CLS;
+    const bool diffuse = (B & PT_MATS_DIFFUSE) && Type == PT_MATERIAL_TYPE_BASIC_DIFFUSE;
+    const bool metal = (B & PT_MATS_METAL) && Type == PT_MATERIAL_TYPE_BASIC_METAL;
+    const bool trans = (B & PT_MATS_TRANSLUCENT) && Type == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT;
+    const bool openpbr = (B & PT_MATS_OPENPBR) && Type == PT_MATERIAL_TYPE_OPENPBR;
     bsdf_material Q;
     Q.Rough = false;
     // HasDirac (basic_metal / basic_translucent .glsl.inc: roughness < 1e-3;
     // OpenPBR: sampling only, HasDirac true).
     bool Dirac = openpbr;
-    if ((MATS & (PT_MATS_METAL | PT_MATS_TRANSLUCENT)) && (metal || trans)) {
+    if ((B & (PT_MATS_METAL | PT_MATS_TRANSLUCENT)) && (metal || trans)) {
         const float Roughness = MaterialTexturableValue(
             S, M, metal ? PT_BASIC_METAL_ROUGHNESS : PT_BASIC_TRANSLUCENT_ROUGHNESS, P.TextureUV);
         const float Anisotropy = MaterialTexturableValue(
@@ -900,7 +903,7 @@ PT_DEV void GenerateNewPath(const dscene& S, const dslots& L, const dframe& F, c
 
 // Scatter (basic_scatter.glsl:114-310).  Returns true if an extension ray was
 // produced (written to O, V).
-template <uint32_t MATS>
+template <uint32_t MATS, uint32_t CLS = 0xFFFFFFFFu>
 PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3& V, uint32_t HitShape,
                     uint32_t HitMaterial, float HitTime, uint32_t PN, uint32_t PT, pt2 UV)
 {
@@ -975,7 +978,7 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
         P.Lambda = Lambda;
         P.ExteriorIOR = ExteriorIOR;
         pt4 T, Pr;
-        if (!SampleSurfaceIntegrand<MATS>(S, G, Nrm, TX, TY, P, Out, In, T, Pr)) return false;
+        if (!SampleSurfaceIntegrand<MATS, CLS>(S, G, Nrm, TX, TY, P, Out, In, T, Pr)) return false;
         float Scale = 1.0f / pt_max(PT_EPSILON, max4(Pr));
         Path.Throughput = Path.Throughput * (T * Scale);
         Path.Probability = Path.Probability * (Pr * Scale);
@@ -1054,9 +1057,68 @@ __global__ __launch_bounds__(256) void restore_rays_kernel(dslots L, dframe F, c
 
 // Ray sources of the extend kernel: the renderer's slots, or the arrays of
 // the ray-query API.
+#if PT_EXP_CLASSQ == 2
+// Experiment build only: the last of a tile's four waves to finish extend
+// appends the tile's 256 positions to the per-class sub-lists t % CQ_SUB
+// (one atomic per class, by lanes 0..C-1 at once).  The waves hand their
+// class ballots over in LDS (lds: [0] a ticket zeroed at kernel start, then
+// 4 x C ballots); no block barrier.
+PT_DEV void ClassListAppend(const dslots& L, uint64_t* lds, uint32_t q, const uint64_t* b)
+{
+    constexpr uint32_t C = PT_OUTCOME_CLASSES;
+    uint64_t* bl = lds + 1;
+    const uint32_t w = (q >> 6) & 3u, lane = q & 63u;
+    uint64_t mine = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < C; c++) if (lane == c) mine = b[c];
+    if (lane < C) bl[w * C + lane] = mine;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    uint32_t old = 0;
+    if (lane == 0) old = atomicAdd(reinterpret_cast<uint32_t*>(lds), 1u);
+    old = (uint32_t)__shfl((int)old, 0, 64);
+    if (old != 3u) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    const uint32_t tile = q >> 8, sub = tile % CQ_SUB;
+    // The ballots are wave-uniform: read into scalar registers.
+    auto U = [&](uint32_t i) -> uint64_t {
+        const uint64_t v = bl[i];
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+        return ((uint64_t)hi << 32) | lo;
+    };
+    uint32_t mycount = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < C; c++) {
+        uint32_t t = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) t += (uint32_t)__popcll(U(k * C + c));
+        if (lane == c) mycount = t;
+    }
+    uint32_t base = 0;
+    if (lane < C && mycount) base = atomicAdd(&L.cq_counts[lane * CQ_SUB + sub], mycount);
+#pragma unroll
+    for (uint32_t c = 0; c < C; c++) {
+        const uint32_t bc = (uint32_t)__shfl((int)base, (int)c, 64);
+        uint32_t before = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint64_t m = U(k * C + c);
+            if ((m >> lane) & 1ull) {
+                const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                L.cq_list[((size_t)c * CQ_SUB + sub) * L.cq_capk + bc + before + r] = tile * 256u + k * 64u + lane;
+            }
+            before += (uint32_t)__popcll(m);
+        }
+    }
+}
+#endif
+
 struct ray_source_slots {
     dslots L;
     dframe F;
+#if PT_EXP_CLASSQ == 2
+    uint64_t* cq_lds = nullptr;
+#endif
     // s is a ray POSITION (TileOrder), not a slot.
     PT_DEV bool load(uint32_t s, pt3& O, pt3& V, float& D) const
     {
@@ -1083,13 +1145,28 @@ struct ray_source_slots {
         if (!classes) {
             uint64_t b = __ballot(cls == PT_OUTCOME_CLASSES - 1);
             if ((q & 63u) == 0) m[4 * (PT_OUTCOME_CLASSES - 1)] = b;
+#if PT_EXP_CLASSQ == 2
+            if (L.cq_list) {
+                const uint64_t bs[PT_OUTCOME_CLASSES] = {~b, 0ull, 0ull, 0ull, b};
+                ClassListAppend(L, cq_lds, q, bs);
+            }
+#endif
             return;
         }
+#if PT_EXP_CLASSQ == 2
+        uint64_t bs[PT_OUTCOME_CLASSES];
+#endif
 #pragma unroll
         for (uint32_t c = 0; c < PT_OUTCOME_CLASSES; c++) {
             uint64_t b = __ballot(cls == c);
             if ((q & 63u) == 0) m[4 * c] = b;
+#if PT_EXP_CLASSQ == 2
+            bs[c] = b;
+#endif
         }
+#if PT_EXP_CLASSQ == 2
+        if (L.cq_list) ClassListAppend(L, cq_lds, q, bs);
+#endif
     }
 };
 
@@ -1225,6 +1302,20 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
             timed = true;
         }
     }
+#if PT_EXP_CLASSQ == 2
+    if constexpr (kRendererSource<Src>) {
+        __shared__ uint64_t cq_lds[1 + 4 * PT_OUTCOME_CLASSES];
+        if (src.L.cq_list) {
+            if (threadIdx.x == 0) cq_lds[0] = 0ull;
+            if (blockIdx.x == 0 && threadIdx.x < PT_OUTCOME_CLASSES * CQ_SUB) src.L.cq_next[threadIdx.x] = 0u;
+            __syncthreads();
+        }
+        Src s2 = src;
+        s2.cq_lds = cq_lds;
+        ExtendTile<Src, SPILL, CAP, E>(S, s2, n, spill, spill_stride, smem, tile, timed, ncache, ncn);
+        return;
+    }
+#endif
     ExtendTile<Src, SPILL, CAP, E>(S, src, n, spill, spill_stride, smem, tile, timed, ncache, ncn);
 }
 
@@ -1480,7 +1571,7 @@ PT_DEV void CompletePath(const dscene& S, const dslots& L, const dframe& F, cons
 // COMPACT: a completed path is left to the block's completion queue (its RNG
 // state, Sample and empty-stack flag in cstate / csample / cactnone); else it
 // is completed here and its new camera ray returned in O, V.
-template <uint32_t MATS, bool COMPACT>
+template <uint32_t MATS, bool COMPACT, uint32_t CLS = 0xFFFFFFFFu>
 PT_DEV void ShadeSlot(const dscene& S, const dslots& L, const dframe& F, const dparams& Pm, uint32_t s, uint32_t p16,
                       uint32_t x, uint32_t y, uint32_t stream, bool valid, pt3& O, pt3& V, bool& completed,
                       uint32_t& cstate, pt3& csample, bool& cactnone)
@@ -1548,7 +1639,7 @@ PT_DEV void ShadeSlot(const dscene& S, const dslots& L, const dframe& F, const d
             PTg = PackUnitVector(TX);
         }
 
-        if (Scatter<MATS>(S, G, Pm.termination_probability, P, O, V, HitShape, HitMaterial, HitTime, PN, PTg, UV)) {
+        if (Scatter<MATS, CLS>(S, G, Pm.termination_probability, P, O, V, HitShape, HitMaterial, HitTime, PN, PTg, UV)) {
             // StorePathVertex of a continuing path: Scatter changes Sample only
             // on escape (which terminates the path) and never Lambda0, so lam
             // is unchanged; the active-shape stack is written when it moved.
@@ -1672,6 +1763,154 @@ __global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void shade_kernel(dscen
     ShadeTile<MATS, COMPACT>(S, L, F, Pm, L.order ? L.order[blockIdx.x] : blockIdx.x);
     ShadeStatsEnd();
 }
+
+#if PT_EXP_CLASSQ
+// Experiment build only: global per-class shade lists.
+// Extend appends every position of a tile to its outcome class's list
+// (ClassListAppend); shade_classq_kernel gives each block 256 entries of one
+// class, so every wave shades one class with that class's BSDF code alone.
+// New rays stay at the position they replace (no TileOrder: the slot <->
+// position map is unchanged), so results are identical.
+#if PT_EXP_CLASSQ == 1
+// PT_EXP_CLASSQ=1: the lists are built by a kernel between extend and shade.
+// A block lists CQ_TILES tiles: one wave scans the (tile, wave word) counts
+// of every class and takes the block's run of each class's list with one
+// atomic per class, lanes 0..C-1 at once (a tile per block instead: 4096
+// atomics per address per C2 round, serialised, 26 us).  Block 0 clears the
+// other parity's counters for the next round.
+constexpr uint32_t CQ_TILES = 16;
+__global__ __launch_bounds__(256) void class_list_kernel(dslots L, uint32_t mat_classes, uint32_t* counts,
+                                                         uint32_t* next_counts, uint32_t* list, uint32_t capk)
+{
+    constexpr uint32_t C = PT_OUTCOME_CLASSES;
+    static_assert(CQ_SUB == 1 && 4 * CQ_TILES <= 64, "one list per class; one wave scans the block's counts");
+    __shared__ uint64_t om_s[CQ_TILES * 4 * C];
+    __shared__ uint32_t off[C][4 * CQ_TILES];
+    __shared__ uint32_t base[C];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint32_t tile0 = blockIdx.x * CQ_TILES;
+    const uint32_t ntiles = L.tile_count - tile0 < CQ_TILES ? L.tile_count - tile0 : CQ_TILES;
+    if (blockIdx.x == 0 && t < C) next_counts[t] = 0u;
+    for (uint32_t i = t; i < ntiles * 4 * C; i += 256) om_s[i] = L.outcome[(size_t)tile0 * (4 * C) + i];
+    __syncthreads();
+    auto mask = [&](uint32_t j, uint32_t c, uint32_t k) -> uint64_t {
+        const uint64_t* om = om_s + j * (4 * C);
+        if (mat_classes) return om[4 * c + k];
+        const uint64_t miss = om[4 * (C - 1) + k];
+        return c == C - 1 ? miss : c == 0 ? ~miss : 0ull;
+    };
+    if (t < 64) {
+        const uint32_t j = t >> 2, k = t & 3u;
+        uint32_t total = 0;
+#pragma unroll
+        for (uint32_t c = 0; c < C; c++) {
+            const uint32_t n = j < ntiles ? (uint32_t)__popcll(mask(j, c, k)) : 0u;
+            uint32_t x = n;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+                if ((int)lane >= o) x += y;
+            }
+            off[c][t] = x - n;
+            const uint32_t xt = (uint32_t)__shfl((int)x, 63, 64);
+            if (lane == c) total = xt;
+        }
+        if (lane < C) base[lane] = total ? atomicAdd(&counts[lane], total) : 0u;
+    }
+    __syncthreads();
+    for (uint32_t j = 0; j < ntiles; j++) {
+        const uint32_t q = (tile0 + j) * 256 + t;
+#pragma unroll
+        for (uint32_t c = 0; c < C; c++) {
+            const uint64_t m = mask(j, c, w);
+            if ((m >> lane) & 1ull) {
+                const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                list[(size_t)c * capk + base[c] + off[c][4 * j + w] + r] = q;
+            }
+        }
+    }
+}
+#endif
+
+template <uint32_t MATS, bool COMPACT>
+__global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void shade_classq_kernel(dscene S, dslots L, dframe F,
+                                                                                         dparams Pm,
+                                                                                         const uint32_t* counts,
+                                                                                         const uint32_t* list,
+                                                                                         uint32_t capk)
+{
+    constexpr uint32_t C = PT_OUTCOME_CLASSES;
+    // Sub-list starts and class totals from the CQ_SUB x C counters
+    // (uniform scalar loads; no barrier).
+    uint32_t pre[C][CQ_SUB], tot[C];
+#pragma unroll
+    for (uint32_t k = 0; k < C; k++) {
+        uint32_t x = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < CQ_SUB; j++) { pre[k][j] = x; x += counts[k * CQ_SUB + j]; }
+        tot[k] = x;
+    }
+    uint32_t c = C, i0 = 0, n = 0, start = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < C; k++) {
+        const uint32_t nk = tot[k];
+        const uint32_t bk = (nk + 255u) / 256u;
+        if (c == C && blockIdx.x < start + bk) { c = k; i0 = (blockIdx.x - start) * 256u; n = nk; }
+        start += bk;
+    }
+    if (c == C) return;   // whole block: past every list
+    const uint32_t i = i0 + threadIdx.x;
+    const bool in = i < n;
+    uint32_t sub = 0, first = 0;   // the last sub-list starting at or before i
+#pragma unroll
+    for (uint32_t k = 0; k < C; k++) {
+        if (k != c) continue;
+#pragma unroll
+        for (uint32_t j = 1; j < CQ_SUB; j++)
+            if (pre[k][j] <= i) { sub = j; first = pre[k][j]; }
+    }
+    const uint32_t q = in ? list[((size_t)c * CQ_SUB + sub) * capk + (i - first)] : 0u;
+    const uint32_t s = (q & ~255u) | L.slotof[q];
+    uint32_t x = 0, y = 0, stream = 0;
+    const bool valid = in && SlotPixel(F, s, x, y, stream);
+    const uint32_t p16 = (q & 255u) << 8;
+    pt3 O = v3s(0), V = v3s(0);
+    bool completed = false;
+    uint32_t cstate = 0;
+    pt3 csample = v3s(0.0f);
+    bool cactnone = false;
+    switch (c) {
+    case 0:
+        ShadeSlot<MATS, COMPACT, PT_MATS_DIFFUSE>(S, L, F, Pm, s, p16, x, y, stream, valid, O, V, completed, cstate,
+                                                  csample, cactnone);
+        break;
+    case 1:
+        ShadeSlot<MATS, COMPACT, PT_MATS_METAL>(S, L, F, Pm, s, p16, x, y, stream, valid, O, V, completed, cstate,
+                                                csample, cactnone);
+        break;
+    case 2:
+        ShadeSlot<MATS, COMPACT, PT_MATS_TRANSLUCENT>(S, L, F, Pm, s, p16, x, y, stream, valid, O, V, completed,
+                                                      cstate, csample, cactnone);
+        break;
+    case PT_OUTCOME_CLASSES - 1:
+        ShadeSlot<MATS, COMPACT, 0u>(S, L, F, Pm, s, p16, x, y, stream, valid, O, V, completed, cstate, csample,
+                                     cactnone);
+        break;
+    default:
+        ShadeSlot<MATS, COMPACT>(S, L, F, Pm, s, p16, x, y, stream, valid, O, V, completed, cstate, csample, cactnone);
+        break;
+    }
+    const uint64_t cm = __ballot(completed);
+    const uint32_t words = L.n / 64;
+    if ((threadIdx.x & 63u) == 0 && cm && words)
+        atomicAdd(&L.done[((blockIdx.x * 256u + threadIdx.x) >> 6) % words], (uint32_t)__popcll(cm));
+    if constexpr (COMPACT) CompletionQueue(S, L, F, Pm, s, completed, cm, cstate, csample, cactnone, O, V);
+    if (valid) {
+        L.ray[q] = make_float4(O.x, O.y, O.z, __uint_as_float(PackUnitVector(V)));
+        L.pos[s] = (uint16_t)(((q & 255u) << 8) | (q & 255u));
+    }
+}
+#endif
 
 
 // One round (extend + shade) of a tile per block, for partitions whose tiles
@@ -2078,6 +2317,46 @@ hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd
     else LaunchShade<false>(S, L, F, P, scene_mats, st);
     return hipGetLastError();
 }
+
+#if PT_EXP_CLASSQ
+template <bool COMPACT>
+static void LaunchShadeQ(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
+                         uint32_t scene_mats, const uint32_t* counts, const uint32_t* list, hipStream_t st)
+{
+    const uint32_t blocks = L.tile_count + ptd::PT_OUTCOME_CLASSES;
+    const uint32_t capk = pt_classq_sub_capacity(L.tile_count);
+    switch (pt_shade_mats(scene_mats)) {
+    case PT_MATS_DIFFUSE | PT_MATS_SCENE:
+        hipLaunchKernelGGL((ptd::shade_classq_kernel<PT_MATS_DIFFUSE | PT_MATS_SCENE, COMPACT>), dim3(blocks), dim3(256),
+                           0, st, S, L, F, P, counts, list, capk);
+        break;
+    case PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_SCENE:
+        hipLaunchKernelGGL((ptd::shade_classq_kernel<PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_SCENE, COMPACT>),
+                           dim3(blocks), dim3(256), 0, st, S, L, F, P, counts, list, capk);
+        break;
+    default:
+        hipLaunchKernelGGL((ptd::shade_classq_kernel<PT_MATS_ALL | PT_MATS_SCENE, COMPACT>), dim3(blocks), dim3(256), 0,
+                           st, S, L, F, P, counts, list, capk);
+        break;
+    }
+}
+
+hipError_t pt_launch_shade_classq(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F,
+                                  const ptd::dparams& P, uint32_t scene_mats, bool compact, uint32_t* counts,
+                                  uint32_t* next_counts, uint32_t* list, hipStream_t st)
+{
+    if (L.n == 0 || L.tile_count == 0) return hipSuccess;
+#if PT_EXP_CLASSQ == 1
+    hipLaunchKernelGGL(ptd::class_list_kernel, dim3((L.tile_count + ptd::CQ_TILES - 1) / ptd::CQ_TILES), dim3(256), 0,
+                       st, L, S.mat_classes, counts, next_counts, list, pt_classq_sub_capacity(L.tile_count));
+#else
+    (void)next_counts;
+#endif
+    if (compact) LaunchShadeQ<true>(S, L, F, P, scene_mats, counts, list, st);
+    else LaunchShadeQ<false>(S, L, F, P, scene_mats, counts, list, st);
+    return hipGetLastError();
+}
+#endif
 
 #if PT_SHADE_STATS
 // Experiment build only (tools/shade_stats.py): the launch-summed shade

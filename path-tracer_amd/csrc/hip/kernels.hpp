@@ -35,6 +35,14 @@ struct dslots {
     uint32_t* spill;    // traversal stack spill: (needed - LDS capacity) rows x n
     uint32_t n;
     uint32_t tile_count;    // n / 256: one block per tile
+#if PT_EXP_CLASSQ
+    // Experiment build only: extend appends each tile's positions to the
+    // per-class sub-lists (counters cq_counts, cleared: cq_next) when set.
+    uint32_t* cq_counts = nullptr;
+    uint32_t* cq_next = nullptr;
+    uint32_t* cq_list = nullptr;
+    uint32_t cq_capk = 0;
+#endif
 };
 
 struct dframe {
@@ -113,6 +121,21 @@ hipError_t pt_launch_resolve(const float4* accum, uint32_t n, float brightness, 
 // paths also end at surfaces.
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
                            uint32_t scene_mats, bool compact, hipStream_t st);
+#if PT_EXP_CLASSQ
+// Experiment build only: shade through global per-class lists, each class's
+// list CQ_SUB sub-lists of pt_classq_sub_capacity words; counts: the
+// PT_OUTCOME_CLASSES x CQ_SUB sub-list counters of this round (next_counts:
+// the other parity's, cleared for the next round).  PT_EXP_CLASSQ=1: a list
+// kernel runs first; 2: the round's extend built them (dslots.cq_*).
+#ifndef PT_CQ_SUB
+#define PT_CQ_SUB (PT_EXP_CLASSQ == 2 ? 8 : 1)
+#endif
+constexpr uint32_t CQ_SUB = PT_CQ_SUB;   // sub-lists per class: tile t appends to t % CQ_SUB
+inline uint32_t pt_classq_sub_capacity(uint32_t tiles) { return (tiles + CQ_SUB - 1) / CQ_SUB * 256; }
+hipError_t pt_launch_shade_classq(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F,
+                                  const ptd::dparams& P, uint32_t scene_mats, bool compact, uint32_t* counts,
+                                  uint32_t* next_counts, uint32_t* list, hipStream_t st);
+#endif
 hipError_t pt_launch_vertex_decode(const uint2* v, uint32_t n, float4* attr, float* vv, hipStream_t st);
 hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st);
 // Fused round (extend + shade per tile in one launch, round_kernel): the

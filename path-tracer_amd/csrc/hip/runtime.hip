@@ -167,6 +167,10 @@ struct pt_basic_renderer {
     bool grey = false;                  // the live paths are in the grey record form (slots.prob1 set)
     bool grey_blocked = false;          // some live path cannot take it (until the next Reset / state write)
     dbuf<uint32_t> grey_count;          // pt_launch_grey_check's result word
+#if PT_EXP_CLASSQ
+    dbuf<uint32_t> cq_counts, cq_list;  // experiment build: per-class shade lists
+    uint32_t cq_parity = 0;
+#endif
     dbuf<float> lam;                    // lambda0 per slot (Sample is 0 between rounds)
     dbuf<float2> uv;
     dbuf<uint2> act;
@@ -1079,6 +1083,9 @@ void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
     if (!r) return;
     if (d) { (void)hipSetDevice(d->id); (void)DeviceWait(d); }
     r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->prob1.release(); r->grey_count.release();
+#if PT_EXP_CLASSQ
+    r->cq_counts.release(); r->cq_list.release();
+#endif
     r->lam.release();
     r->uv.release(); r->act.release(); r->pos.release(); r->slotof.release(); r->outcome.release();
     r->tilecost.release(); r->order.release();
@@ -1209,11 +1216,35 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
             PT_HIP(pt_launch_round(r->scene->d, L, F, P, ShadeMats(r), d->stream));
             if (int e = EndTimed(d, ep)) return e;
         } else {
+#if PT_EXP_CLASSQ
+            const size_t nc = (size_t)ptd::PT_OUTCOME_CLASSES * CQ_SUB;
+            if (!r->cq_list.ptr) {
+                if (r->cq_counts.alloc(2 * nc) != hipSuccess ||
+                    r->cq_list.alloc(nc * pt_classq_sub_capacity(L.tile_count)) != hipSuccess ||
+                    hipMemset(r->cq_counts.ptr, 0, 2 * nc * sizeof(uint32_t)) != hipSuccess) {
+                    SetError("class list allocation failed");
+                    return -1;
+                }
+            }
+            ptd::dslots LQ = L;
+            LQ.cq_counts = r->cq_counts.ptr + nc * r->cq_parity;
+            LQ.cq_next = r->cq_counts.ptr + nc * (r->cq_parity ^ 1u);
+            LQ.cq_list = r->cq_list.ptr;
+            LQ.cq_capk = pt_classq_sub_capacity(L.tile_count);
+            r->cq_parity ^= 1u;
+            if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled)) return e;
+            PT_HIP(pt_launch_extend(r->scene->d, PT_EXP_CLASSQ == 2 ? LQ : L, F, L.spill, d->stream));
+            if (int e = EndTimed(d, ep)) return e;
+            if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled)) return e;
+            PT_HIP(pt_launch_shade_classq(r->scene->d, L, F, P, ShadeMats(r), ShadeCompact(r), LQ.cq_counts,
+                                          LQ.cq_next, r->cq_list.ptr, d->stream));
+#else
             if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled)) return e;
             PT_HIP(pt_launch_extend(r->scene->d, L, F, L.spill, d->stream));
             if (int e = EndTimed(d, ep)) return e;
             if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled)) return e;
             PT_HIP(pt_launch_shade(r->scene->d, L, F, P, ShadeMats(r), ShadeCompact(r), d->stream));
+#endif
             if (int e = EndTimed(d, ep)) return e;
         }
         if (sort) PT_HIP(pt_launch_tile_order(L, d->stream));
