@@ -209,6 +209,8 @@ def main():
                     help="every rank on device 0 (multi-rank flow check on a one-GPU box; timings not meaningful)")
     ap.add_argument("--launch-check", action="store_true",
                     help="N-rank launch plumbing only (gloo, no GPU): CPU test of the launcher")
+    ap.add_argument("--split", type=int, default=0,
+                    help="tile groups on concurrent streams (ptSetBasicRendererSplit): 0 automatic, 1 off, K")
     ap.add_argument("--streams", type=int, default=0,
                     help="path streams per owned pixel (0: auto -- bands fill ~2^21 slots per launch, samples 1)")
     ap.add_argument("--inject-failure", type=int, default=-1, metavar="RANK",
@@ -269,6 +271,11 @@ def main():
     if shard == "samples":
         r.FrameIndex = rank << 24
     slots_owned = px_owned * streams    # paths (rays) per round
+    # Tile groups on concurrent streams (ptSetBasicRendererSplit): profiling
+    # times group 0's launches, which cover timed_tiles of the tiles.
+    r.set_split(args.split)
+    split = r.split()
+    launch_slots = slots_owned * split["timed_tiles"] / max(split["tiles"], 1) if split["groups"] > 1 else slots_owned
     # This rank's frame target (Σ alpha): samples -> 1/N of spp x frame,
     # bands -> spp x its own pixels.
     target = math.ceil(spp * width * height / world) if shard == "samples" else spp * px_owned
@@ -374,12 +381,10 @@ def main():
     if not args.no_steady:
         r.reset()
         r.run(2)
-        for _ in range(SETTLE_ROUNDS):
-            r.run(1)
+        r.run_rounds(SETTLE_ROUNDS)     # consecutive Run(1) rounds, as the frames run them
         dev.synchronize()
         s0 = time.perf_counter()
-        for _ in range(STEADY_ROUNDS):
-            r.run(1)
+        r.run_rounds(STEADY_ROUNDS)
         dev.synchronize()
         sdt = time.perf_counter() - s0
         steady = {"rounds": STEADY_ROUNDS, "after_rounds": SETTLE_ROUNDS + 2,
@@ -420,7 +425,7 @@ def main():
     for name, (n_k, ms_k, rounds_k) in kstats.items():
         if n_k:
             avg = ms_k / max(rounds_k, 1)   # per round (= per launch except for round batches)
-            kernels[name] = {"avg_ms": avg, "gbps": ALG_BYTES[name] * slots_owned / (avg * 1e-3) / 1e9,
+            kernels[name] = {"avg_ms": avg, "gbps": ALG_BYTES[name] * launch_slots / (avg * 1e-3) / 1e9,
                              "launches": n_k, "rounds": rounds_k}
     # traversal-level cache rate below: extend's time per round, or the fused kernels'
     avg_ext = next(kernels[k]["avg_ms"] for k in ("extend", "round", "rounds") if k in kernels)
@@ -497,6 +502,7 @@ def main():
             "spp_target": spp,
             "streams": streams,
             "slots_per_launch_rank0": slots_owned,
+            "split": split["groups"],
             "frame_target_samples_rank0": target,
             "mesh_faces": info.mesh_face_count,
             "image_identity": identity,
@@ -525,7 +531,13 @@ def main():
             "traffic": traffic,
             "traffic_unit": "bytes per launch (HBM, PMC)",
             "traffic_source": prof.get("profile") if traffic is not None else None,
-            "alg_bytes_per_launch": ALG_BYTES[dom] * slots_owned,
+            "alg_bytes_per_launch": round(ALG_BYTES[dom] * launch_slots),
+            # Tile groups: that many launches of each kernel run concurrently
+            # per round (one per group's stream); a launch covers
+            # slots_per_timed_launch slots, and its rate is its own bytes over
+            # its own duration (path_frac is the whole frame's).
+            "split_groups": split["groups"],
+            "slots_per_timed_launch": round(launch_slots),
             "alg_bytes_per_slot": ALG_BYTES[dom],
             "launch_avg_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
             "launches_timed": {**{k: v[0] for k, v in kstats.items()}, "every_nth_round": args.profile_period},
@@ -560,7 +572,7 @@ def main():
         "faces_per_ray": round(trav["faces_per_ray"], 2),
         "pops_per_ray": round(trav["pops_per_ray"], 2),
         "cache_bytes_per_ray": round(cache_bytes, 1),
-        "cache_gbps": round(cache_bytes * slots_owned / (avg_ext * 1e-3) / 1e9, 1),
+        "cache_gbps": round(cache_bytes * launch_slots / (avg_ext * 1e-3) / 1e9, 1),
         "l2_peak_gbps": L2_PEAK_GBPS,
     }
     if not args.no_cpu_baseline and world == 1:   # rank 0 at N=1 only

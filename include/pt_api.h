@@ -242,6 +242,22 @@ int                ptSetBasicRendererFusedRounds(pt_basic_renderer* renderer, in
  * Default 0.  ptRenderFrame runs its Run(1) rounds this way. */
 int                ptRunBasicRendererRounds(pt_device* device, pt_basic_renderer* renderer, uint32_t count);
 int                ptSetBasicRendererRoundBatch(pt_basic_renderer* renderer, uint32_t rounds);
+/* Tile groups on concurrent streams (no reference counterpart: a launch
+ * schedule).  Consecutive rounds that run one launch pair per round
+ * (ptRunBasicRendererRounds, ptRenderFrame) split the renderer's tiles into K
+ * groups (tile t in group t % K); each group runs the batch's rounds on its
+ * own HIP stream, so one group's launches fill the CUs another group's
+ * kernel tail leaves idle.  The device stream forks before the batch and
+ * joins after it, and every wait covers the groups.  Results are identical
+ * for every K.  groups: 0 = automatic (2 when the rounds run unfused over at
+ * least 2 048 tiles, else 1), 1 = off, 2..PT_MAX_SPLIT = that many.
+ * ptGetBasicRendererSplit reports the K that consecutive rounds use now, the
+ * tiles of group 0 (the launches kernel profiling times) and all tiles; any
+ * pointer may be NULL.  Default 0. */
+#define PT_MAX_SPLIT 4
+int                ptSetBasicRendererSplit(pt_basic_renderer* renderer, uint32_t groups);
+int                ptGetBasicRendererSplit(const pt_basic_renderer* renderer, uint32_t* groups, uint32_t* timed_tiles,
+                                           uint32_t* tiles);
 /* OpenPBR shading (opt-in extension, no reference counterpart): 0 (default)
  * = an OpenPBR hit ends its path with no contribution, as in the reference,
  * whose integrator does not compile its OpenPBR BSDF (scene.glsl.inc:685);

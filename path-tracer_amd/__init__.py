@@ -19,7 +19,7 @@ from .integrator import (Device, DeviceScene, SampleBuffer, BasicRenderer, Comm,
 from ._native import (PREVIEW_RENDER_MODE_BASE_COLOR, PREVIEW_RENDER_MODE_BASE_COLOR_SHADED, PREVIEW_RENDER_MODE_NORMAL,
                       PREVIEW_RENDER_MODE_MATERIAL_INDEX, PREVIEW_RENDER_MODE_PRIMITIVE_INDEX,
                       PREVIEW_RENDER_MODE_MESH_COMPLEXITY, PREVIEW_RENDER_MODE_SCENE_COMPLEXITY)
-from ._native import TONE_MAPPING_CLAMP, TONE_MAPPING_REINHARD, TONE_MAPPING_HABLE, TONE_MAPPING_ACES
+from ._native import TONE_MAPPING_CLAMP, TONE_MAPPING_REINHARD, TONE_MAPPING_HABLE, TONE_MAPPING_ACES, MAX_SPLIT
 from ._native import (SHADE_DIFFUSE, SHADE_METAL, SHADE_TRANSLUCENT, SHADE_SCATTER, SHADE_OPENPBR, SHADE_PRIMS,
                       SHADE_SKY, SHADE_TEXWRAP)
 from .image import write_png, write_ppm, write_pfm, read_png

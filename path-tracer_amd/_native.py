@@ -155,6 +155,7 @@ TONE_MAPPING_CLAMP, TONE_MAPPING_REINHARD, TONE_MAPPING_HABLE, TONE_MAPPING_ACES
 KERNEL_PREVIEW = 4
 KERNEL_ROUND = 5     # fused extend + shade (partitions that fit the GPU at once)
 KERNEL_ROUNDS = 6    # a round batch: several rounds of every tile in one launch (PT_KERNEL_ROUNDS)
+MAX_SPLIT = 4        # PT_MAX_SPLIT: tile groups of ptSetBasicRendererSplit
 
 _vp = C.c_void_p
 _u32 = C.c_uint32
@@ -257,6 +258,8 @@ HIP_API = {
     "ptSetBasicRendererFusedRounds": (_i32, [_vp, _i32]),
     "ptRunBasicRendererRounds": (_i32, [_vp, _vp, _u32]),
     "ptSetBasicRendererRoundBatch": (_i32, [_vp, _u32]),
+    "ptSetBasicRendererSplit": (_i32, [_vp, _u32]),
+    "ptGetBasicRendererSplit": (_i32, [_vp, _u32ptr, _u32ptr, _u32ptr]),
     "ptSetBasicRendererOpenPBR": (_i32, [_vp, _i32]),
     "ptGetStats": (_i32, [_vp, _vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "ptTraceRaysStats": (_i32, [_vp, _vp, _u32, _fptr, _u32ptr, _fptr, C.POINTER(C.c_uint64), _vp]),

@@ -1323,8 +1323,14 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
 // wave's time, descending, by a one-block counting sort over 512 log-spaced
 // buckets (16 per octave).  Any order gives the same results; only the
 // kernel's tail changes.
-__global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, uint32_t* order, uint32_t tiles)
+//
+// Tile groups (ptSetBasicRendererSplit): group g of K owns the tiles
+// t = g, g + K, ... and its segment order[start, start + count) of the
+// dispatch order, which it sorts on its own stream; K = 1 is the whole frame.
+__global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, uint32_t* order, uint32_t tiles,
+                                                          uint32_t groups, uint32_t group, uint32_t start)
 {
+    const uint32_t nt = group < tiles ? (tiles - group + groups - 1) / groups : 0u;
     __shared__ uint32_t count[512];
     for (uint32_t i = threadIdx.x; i < 512; i += 1024) count[i] = 0;
     __syncthreads();
@@ -1336,7 +1342,7 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, 
         uint32_t k = min(e * 16u + m, 511u);
         return 511u - k;                                       // longest first
     };
-    for (uint32_t t = threadIdx.x; t < tiles; t += 1024) atomicAdd(&count[key(t)], 1u);
+    for (uint32_t i = threadIdx.x; i < nt; i += 1024) atomicAdd(&count[key(group + i * groups)], 1u);
     __syncthreads();
     // Exclusive scan of the 512 buckets: eight waves scan 64 each with
     // shuffles, then add the totals of the waves before them (a serial scan
@@ -1359,7 +1365,10 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, 
         count[threadIdx.x] = before + incl - c;
     }
     __syncthreads();
-    for (uint32_t t = threadIdx.x; t < tiles; t += 1024) order[atomicAdd(&count[key(t)], 1u)] = t;
+    for (uint32_t i = threadIdx.x; i < nt; i += 1024) {
+        const uint32_t t = group + i * groups;
+        order[start + atomicAdd(&count[key(t)], 1u)] = t;
+    }
 }
 
 // Mesh vertices decoded once per upload for HitAttributes: the octahedral
@@ -2112,10 +2121,11 @@ hipError_t pt_launch_vertex_decode(const uint2* v, uint32_t n, float4* attr, flo
     return hipGetLastError();
 }
 
-hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st)
+hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st, uint32_t groups, uint32_t group)
 {
-    if (!L.order || L.tile_count == 0) return hipSuccess;
-    hipLaunchKernelGGL(ptd::tile_order_kernel, dim3(1), dim3(1024), 0, st, L.tilecost, L.order, L.tile_count);
+    if (!L.order || L.tile_count == 0 || groups == 0 || group >= groups) return hipSuccess;
+    hipLaunchKernelGGL(ptd::tile_order_kernel, dim3(1), dim3(1024), 0, st, L.tilecost, L.order, L.tile_count, groups,
+                       group, pt_tile_group_start(L.tile_count, groups, group));
     return hipGetLastError();
 }
 

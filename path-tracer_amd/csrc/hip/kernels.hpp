@@ -137,7 +137,21 @@ hipError_t pt_launch_shade_classq(const ptd::dscene& S, const ptd::dslots& L, co
                                   uint32_t* next_counts, uint32_t* list, hipStream_t st);
 #endif
 hipError_t pt_launch_vertex_decode(const uint2* v, uint32_t n, float4* attr, float* vv, hipStream_t st);
-hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st);
+// Tile groups (ptSetBasicRendererSplit): group g of K owns tiles g, g + K, ...
+// (pt_tile_group_count of them) and the dispatch-order segment starting at
+// pt_tile_group_start.  pt_launch_tile_order sorts one group's segment
+// longest-first (groups = 1: the whole frame).
+inline uint32_t pt_tile_group_count(uint32_t tiles, uint32_t groups, uint32_t group)
+{
+    return group < tiles ? (tiles - group + groups - 1) / groups : 0u;
+}
+inline uint32_t pt_tile_group_start(uint32_t tiles, uint32_t groups, uint32_t group)
+{
+    uint32_t s = 0;
+    for (uint32_t h = 0; h < group; h++) s += pt_tile_group_count(tiles, groups, h);
+    return s;
+}
+hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st, uint32_t groups = 1, uint32_t group = 0);
 // Fused round (extend + shade per tile in one launch, round_kernel): the
 // tiles the GPU can hold at once for this scene (0: not available), and the
 // launch (hipErrorNotSupported when the scene needs a spilled stack).

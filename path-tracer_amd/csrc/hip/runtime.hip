@@ -98,6 +98,12 @@ struct pt_device {
     uint64_t launches[PT_KERNEL_COUNT] = {};
     uint64_t rounds[PT_KERNEL_COUNT] = {};    // rounds the timed launches covered (a batch: its rounds)
     double total_ms[PT_KERNEL_COUNT] = {};
+    // Tile-group streams (ptSetBasicRendererSplit): groups 1.. of a batch of
+    // rounds run on these, forked from `stream` and joined back into it, so
+    // every wait on `stream` covers them.  Created on first use.
+    hipStream_t group_stream[PT_MAX_SPLIT - 1] = {};
+    hipEvent_t fork_event = nullptr;
+    hipEvent_t join_event[PT_MAX_SPLIT - 1] = {};
 };
 
 struct pt_scene {
@@ -183,6 +189,8 @@ struct pt_basic_renderer {
     int fused = 1;                      // fused rounds mode (ptSetBasicRendererFusedRounds)
     int openpbr = 0;                    // shade OpenPBR materials (ptSetBasicRendererOpenPBR)
     uint32_t round_batch = 0;           // rounds per launch of consecutive Run(1) rounds (0: automatic)
+    uint32_t split = 0;                 // tile groups of consecutive rounds (ptSetBasicRendererSplit): 0 auto, 1 off
+    uint32_t order_groups = 1;          // the group structure the order array holds (tile_order_kernel)
     uint64_t pixels = 0;                // image pixels owned
     uint32_t streams = 1;               // path streams per owned pixel (ptCreateBasicRendererStreams)
     uint32_t stream_tiles = 0;          // tiles per stream
@@ -513,6 +521,11 @@ void ptDestroyDevice(pt_device* d)
     d->comms.clear();
     for (auto& ep : d->pending) { (void)hipEventDestroy(ep.a); (void)hipEventDestroy(ep.b); }
     for (auto& ep : d->free_events) { (void)hipEventDestroy(ep.a); (void)hipEventDestroy(ep.b); }
+    for (uint32_t g = 0; g + 1 < PT_MAX_SPLIT; g++) {
+        if (d->group_stream[g]) (void)hipStreamDestroy(d->group_stream[g]);
+        if (d->join_event[g]) (void)hipEventDestroy(d->join_event[g]);
+    }
+    if (d->fork_event) (void)hipEventDestroy(d->fork_event);
     (void)hipStreamDestroy(d->stream);
     delete d;
 }
@@ -1247,10 +1260,113 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
 #endif
             if (int e = EndTimed(d, ep)) return e;
         }
-        if (sort) PT_HIP(pt_launch_tile_order(L, d->stream));
+        if (sort)
+            for (uint32_t g = 0; g < r->order_groups; g++) PT_HIP(pt_launch_tile_order(L, d->stream, r->order_groups, g));
         r->rays += r->valid_slots;
     }
     return 0;
+}
+
+// Tile groups on concurrent streams (ptSetBasicRendererSplit).  A batch of
+// consecutive rounds over a whole frame ends each extend and shade launch
+// with a tail of a few long blocks while most CUs idle.  Split into K groups
+// of tiles (t = g, g + K, ...), each running its own sequence of rounds on
+// its own stream, the launches of one group fill the CUs another group's
+// tail leaves idle.  A slot's round depends only on its own previous round
+// and the round's FrameIndex, so the results are those of the unsplit
+// rounds, bit for bit.  Measured (tools/exp_two_streams.py, profiles/r05_split):
+// C3 +4 %, C2 and C5 +13 % with two groups; halving the launches on ONE
+// stream costs 14-20 %, so the gain is the overlap.
+constexpr uint32_t SPLIT_MIN_TILES = 2048;   // automatic mode: whole frames (C2 has 4 096 tiles)
+
+static uint32_t SplitGroups(const pt_basic_renderer* r)
+{
+    const ptd::dslots& L = r->slots;
+    if (!L.order || L.tile_count < 2 || r->split == 1) return 1;
+    if (r->split >= 2) return std::min(r->split, L.tile_count);
+    return (!RoundFused(r, L) && L.tile_count >= SPLIT_MIN_TILES) ? 2u : 1u;
+}
+
+// The dispatch order holds each group's tiles in its own segment; a change of
+// K restarts it from the natural order of each group.
+static int EnsureOrderGroups(pt_device* d, pt_basic_renderer* r, uint32_t K)
+{
+    if (r->order_groups == K || !r->slots.order) return 0;
+    const uint32_t T = r->slots.tile_count;
+    std::vector<uint32_t> order(T);
+    uint32_t i = 0;
+    for (uint32_t g = 0; g < K; g++)
+        for (uint32_t t = g; t < T; t += K) order[i++] = t;
+    PT_WAIT(d);
+    PT_HIP(hipMemcpy(r->order.ptr, order.data(), (size_t)T * 4, hipMemcpyHostToDevice));
+    r->order_groups = K;
+    return 0;
+}
+
+static int EnsureGroupStreams(pt_device* d, uint32_t K)
+{
+    if (!d->fork_event) PT_HIP(hipEventCreateWithFlags(&d->fork_event, hipEventDisableTiming));
+    for (uint32_t g = 0; g + 1 < K; g++) {
+        if (!d->group_stream[g]) PT_HIP(hipStreamCreateWithFlags(&d->group_stream[g], hipStreamNonBlocking));
+        if (!d->join_event[g]) PT_HIP(hipEventCreateWithFlags(&d->join_event[g], hipEventDisableTiming));
+    }
+    return 0;
+}
+
+// k consecutive rounds (FrameIndex + 1 ... + k) in K tile groups.  Group 0
+// runs on the device stream (its launches are the ones profiling times);
+// the others wait for everything enqueued before (fork) and the device
+// stream waits for them at the end (join), on every path out.
+static int RunRoundsSplit(pt_device* d, pt_basic_renderer* r, uint64_t k, uint32_t K)
+{
+    PT_HIP(hipSetDevice(d->id));
+    if (int e = EnsureSpill(r)) return e;
+    if (int e = SyncRecordForm(d, r)) return e;
+    if (int e = EnsureOrderGroups(d, r, K)) return e;
+    if (int e = EnsureGroupStreams(d, K)) return e;
+    const ptd::dframe F = Frame(r);
+    const uint32_t mats = ShadeMats(r);
+    const bool compact = ShadeCompact(r);
+    ptd::dslots G[PT_MAX_SPLIT];
+    hipStream_t S[PT_MAX_SPLIT];
+    for (uint32_t g = 0; g < K; g++) {
+        G[g] = r->slots;
+        G[g].order = r->slots.order + pt_tile_group_start(r->slots.tile_count, K, g);
+        G[g].tile_count = pt_tile_group_count(r->slots.tile_count, K, g);
+        S[g] = g ? d->group_stream[g - 1] : d->stream;
+    }
+    PT_HIP(hipEventRecord(d->fork_event, d->stream));
+    for (uint32_t g = 1; g < K; g++) PT_HIP(hipStreamWaitEvent(S[g], d->fork_event, 0));
+    auto rounds = [&]() -> int {
+        for (uint64_t i = 0; i < k; i++) {
+            r->params.FrameIndex += 1;
+            const ptd::dparams P = Params(r, r->params.FrameIndex);
+            const bool sampled = d->profiling && (d->run_tick++ % d->profile_period) == 0;
+            const bool sort = (r->order_tick++ % TILE_ORDER_PERIOD) == 0;
+            for (uint32_t g = 0; g < K; g++) {
+                event_pair ep{};
+                if (g == 0)
+                    if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled)) return e;
+                PT_HIP(pt_launch_extend(r->scene->d, G[g], F, r->slots.spill, S[g]));
+                if (g == 0) {
+                    if (int e = EndTimed(d, ep)) return e;
+                    if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled)) return e;
+                }
+                PT_HIP(pt_launch_shade(r->scene->d, G[g], F, P, mats, compact, S[g]));
+                if (g == 0)
+                    if (int e = EndTimed(d, ep)) return e;
+                if (sort) PT_HIP(pt_launch_tile_order(r->slots, S[g], K, g));
+            }
+            r->rays += r->valid_slots;
+        }
+        return 0;
+    };
+    const int rc = rounds();
+    for (uint32_t g = 1; g < K; g++) {
+        PT_HIP(hipEventRecord(d->join_event[g - 1], S[g]));
+        PT_HIP(hipStreamWaitEvent(d->stream, d->join_event[g - 1], 0));
+    }
+    return rc;
 }
 
 // k consecutive Run(1) calls: the same rounds with the same seeds (FrameIndex
@@ -1288,13 +1404,16 @@ static int RunRounds(pt_device* d, pt_basic_renderer* r, uint64_t k)
                 PT_HIP(pt_launch_rounds(r->scene->d, r->slots, F, P, ShadeMats(r), d->stream));
                 if (int e = EndTimed(d, ep)) return e;
                 // The batch's block times order the next batch.
-                if (r->slots.order) PT_HIP(pt_launch_tile_order(r->slots, d->stream));
+                for (uint32_t g = 0; g < r->order_groups; g++)
+                    PT_HIP(pt_launch_tile_order(r->slots, d->stream, r->order_groups, g));
                 r->rays += r->valid_slots * n;
                 k -= n;
             }
             return 0;
         }
     }
+    const uint32_t K = SplitGroups(r);
+    if (K > 1 && k > 1) return RunRoundsSplit(d, r, k, K);
     for (uint64_t i = 0; i < k; i++)
         if (int e = ptRunBasicRenderer(d, r, 1)) return e;
     return 0;
@@ -1311,6 +1430,26 @@ int ptSetBasicRendererRoundBatch(pt_basic_renderer* r, uint32_t rounds)
 {
     if (!r) { SetError("ptSetBasicRendererRoundBatch: null renderer"); return -1; }
     r->round_batch = rounds;
+    return 0;
+}
+
+int ptSetBasicRendererSplit(pt_basic_renderer* r, uint32_t groups)
+{
+    if (!r || groups > PT_MAX_SPLIT) {
+        SetError("ptSetBasicRendererSplit: bad argument (groups 0..%u)", PT_MAX_SPLIT);
+        return -1;
+    }
+    r->split = groups;
+    return 0;
+}
+
+int ptGetBasicRendererSplit(const pt_basic_renderer* r, uint32_t* groups, uint32_t* timed_tiles, uint32_t* tiles)
+{
+    if (!r) { SetError("ptGetBasicRendererSplit: null renderer"); return -1; }
+    const uint32_t K = SplitGroups(r);
+    if (groups) *groups = K;
+    if (timed_tiles) *timed_tiles = pt_tile_group_count(r->slots.tile_count, K, 0);
+    if (tiles) *tiles = r->slots.tile_count;
     return 0;
 }
 

@@ -280,6 +280,21 @@ class BasicRenderer:
         once), 1 never (one launch per round), R >= 2 always R."""
         _check(N.hip_lib().ptSetBasicRendererRoundBatch(self._h, int(rounds)), "ptSetBasicRendererRoundBatch")
 
+    def set_split(self, groups: int):
+        """Tile groups of consecutive rounds, each on its own HIP stream
+        (ptSetBasicRendererSplit): 0 automatic, 1 off, 2..MAX_SPLIT that many.
+        Results are identical for every value."""
+        _check(N.hip_lib().ptSetBasicRendererSplit(self._h, int(groups)), "ptSetBasicRendererSplit")
+
+    def split(self) -> dict:
+        """{groups, timed_tiles, tiles}: the tile groups consecutive rounds use
+        now, group 0's tiles (the launches kernel profiling times) and all
+        tiles (ptGetBasicRendererSplit)."""
+        g, t0, t = C.c_uint32(0), C.c_uint32(0), C.c_uint32(0)
+        _check(N.hip_lib().ptGetBasicRendererSplit(self._h, C.byref(g), C.byref(t0), C.byref(t)),
+               "ptGetBasicRendererSplit")
+        return {"groups": int(g.value), "timed_tiles": int(t0.value), "tiles": int(t.value)}
+
     def run_rounds(self, count: int):
         """count consecutive Run(1) calls (one new FrameIndex each), batched
         per set_round_batch (ptRunBasicRendererRounds)."""

@@ -5,15 +5,15 @@ kernel tails with the other half's work?
 Renders C3 rounds three ways, after settling each renderer for --settle
 rounds:
   full   one renderer, the whole frame, one stream (the bench's layout);
-  serial two band renderers (16-row bands, rank 0 / 1 of 2) on ONE device:
+  serial2 two band renderers (16-row bands, rank 0 / 1 of 2) on ONE device:
          the same work in two launches per kernel, one stream;
-  two    the same two band renderers, each on its own device (stream).
+  streamsN N band renderers (rank k of N), each on its own device (stream).
 Each is timed over --rounds Run(1) rounds per renderer (enqueued alternately,
 one synchronize at the end); rays = rounds x slots.  Any partition gives the
 same per-slot results (the band split is bit-exact per pixel), so this only
 measures throughput.
 
-usage: python tools/exp_two_streams.py [--config 3] [--settle 34] [--rounds 64]
+usage: python tools/exp_two_streams.py [--config 3] [--settle 34] [--rounds 64] [--parts 2,3,4]
 """
 import argparse
 import json
@@ -30,7 +30,9 @@ def main():
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--settle", type=int, default=34)
     ap.add_argument("--rounds", type=int, default=64)
+    ap.add_argument("--parts", default="2,3,4", help="band partitions, one device (stream) each")
     a = ap.parse_args()
+    a.parts = [int(x) for x in a.parts.split(",")]
     import bench
     pt = bench.load_package()
     scene = pt.Scene.config(a.config)
@@ -66,23 +68,26 @@ def main():
                 "ms_per_round": round(dt / a.rounds * 1e3, 4)}
 
     out = {"config": a.config, "settle": a.settle, "rounds": a.rounds}
-    devA = pt.Device(0)
-    devB = pt.Device(0)
-    full = make(devA, 0, 1)
+    devs = [pt.Device(0) for _ in range(max(a.parts))]
+    made = []
+    full = make(devs[0], 0, 1)
+    made.append(full)
     out["full"] = timed([full])
-    out["full_again"] = timed([full])
-    s0, s1 = make(devA, 0, 2), make(devA, 1, 2)
-    out["serial"] = timed([s0, s1])
-    t1 = make(devB, 1, 2)
-    out["two"] = timed([s0, t1])
-    out["full_last"] = timed([full])
+    s0, s1 = make(devs[0], 0, 2), make(devs[0], 1, 2)
+    made += [s0, s1]
+    out["serial2"] = timed([s0, s1])
+    for n in a.parts:
+        parts = [make(devs[k], k, n) for k in range(n)]
+        made += parts
+        out[f"streams{n}"] = timed(parts)
+        out["full_again"] = timed([full])
     print(json.dumps(out))
-    for r, keep in (full, s0, s1, t1):
+    for r, keep in made:
         r.close()
         for k in keep:
             k.close()
-    devB.close()
-    devA.close()
+    for d in devs:
+        d.close()
 
 
 if __name__ == "__main__":
