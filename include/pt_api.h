@@ -249,8 +249,9 @@ int                ptSetBasicRendererRoundBatch(pt_basic_renderer* renderer, uin
  * own HIP stream, so one group's launches fill the CUs another group's
  * kernel tail leaves idle.  The device stream forks before the batch and
  * joins after it, and every wait covers the groups.  Results are identical
- * for every K.  groups: 0 = automatic (2 when the rounds run unfused over at
- * least 2 048 tiles, else 1), 1 = off, 2..PT_MAX_SPLIT = that many.
+ * for every K.  groups: 0 = automatic (3 when the rounds run unfused over at
+ * least 2 048 tiles, else 1), 1 = off, 2..PT_MAX_SPLIT = that many (4 takes
+ * every hardware queue of the process and measured slower).
  * ptGetBasicRendererSplit reports the K that consecutive rounds use now, the
  * tiles of group 0 (the launches kernel profiling times) and all tiles; any
  * pointer may be NULL.  Default 0. */

@@ -1274,17 +1274,21 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
 // its own stream, the launches of one group fill the CUs another group's
 // tail leaves idle.  A slot's round depends only on its own previous round
 // and the round's FrameIndex, so the results are those of the unsplit
-// rounds, bit for bit.  Measured (tools/exp_two_streams.py, profiles/r05_split):
-// C3 +4 %, C2 and C5 +13 % with two groups; halving the launches on ONE
-// stream costs 14-20 %, so the gain is the overlap.
+// rounds, bit for bit.  Measured (bench.py A/B, profiles/r05_split,
+// r05_splitk): K = 2 / 3 / 4 against 1 -- C3 +4.8 / +6.8 / -8 %, C2 +17 /
+// +17 / -3 %, C5 +15 / +16 / -11 %, C4 +1.3 / +1.7 / -1 %; halving the
+// launches on ONE stream costs 14-20 % (tools/exp_two_streams.py), so the
+// gain is the overlap.  Four groups take every hardware queue of the
+// process (GPU_MAX_HW_QUEUES = 4) and lose.
 constexpr uint32_t SPLIT_MIN_TILES = 2048;   // automatic mode: whole frames (C2 has 4 096 tiles)
+constexpr uint32_t SPLIT_AUTO_GROUPS = 3;
 
 static uint32_t SplitGroups(const pt_basic_renderer* r)
 {
     const ptd::dslots& L = r->slots;
     if (!L.order || L.tile_count < 2 || r->split == 1) return 1;
     if (r->split >= 2) return std::min(r->split, L.tile_count);
-    return (!RoundFused(r, L) && L.tile_count >= SPLIT_MIN_TILES) ? 2u : 1u;
+    return (!RoundFused(r, L) && L.tile_count >= SPLIT_MIN_TILES) ? SPLIT_AUTO_GROUPS : 1u;
 }
 
 // The dispatch order holds each group's tiles in its own segment; a change of

@@ -87,7 +87,7 @@ def test_split_equals_unsplit_and_oracle(pt, dev, config, W, H, batches):
 
 @pytest.mark.parametrize("config,W,H,spp", [(2, 1024, 1024, 4), (5, 2048, 1024, 2), (3, 1920, 1080, 2)])
 def test_automatic_split_full_frames(pt, dev, config, W, H, spp):
-    """The configs' full frames take two groups automatically; a
+    """The configs' full frames take three groups automatically; a
     ptRenderFrame with them equals the unsplit frame bit for bit."""
     s = scene_for(pt, config)
     ds = pt.DeviceScene(dev)
@@ -102,8 +102,8 @@ def test_automatic_split_full_frames(pt, dev, config, W, H, spp):
         r.set_split(k)
         sp = r.split()
         if k == 0:
-            assert sp["groups"] == 2 and sp["tiles"] >= 2048, sp
-            assert sp["timed_tiles"] == (sp["tiles"] + 1) // 2
+            assert sp["groups"] == 3 and sp["tiles"] >= 2048, sp
+            assert sp["timed_tiles"] == (sp["tiles"] + 2) // 3
         else:
             assert sp["groups"] == 1
         rounds, samples = r.render_frame(spp * W * H)
