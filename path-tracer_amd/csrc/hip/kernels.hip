@@ -1330,7 +1330,7 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
 __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, uint32_t* order, uint32_t tiles,
                                                           uint32_t groups, uint32_t group, uint32_t start)
 {
-    const uint32_t nt = group < tiles ? (tiles - group + groups - 1) / groups : 0u;
+    const uint32_t nt = pt_tile_group_count(tiles, groups, group);
     __shared__ uint32_t count[512];
     for (uint32_t i = threadIdx.x; i < 512; i += 1024) count[i] = 0;
     __syncthreads();
@@ -1342,7 +1342,7 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, 
         uint32_t k = min(e * 16u + m, 511u);
         return 511u - k;                                       // longest first
     };
-    for (uint32_t i = threadIdx.x; i < nt; i += 1024) atomicAdd(&count[key(group + i * groups)], 1u);
+    for (uint32_t i = threadIdx.x; i < nt; i += 1024) atomicAdd(&count[key(pt_tile_group_tile(tiles, groups, group, i))], 1u);
     __syncthreads();
     // Exclusive scan of the 512 buckets: eight waves scan 64 each with
     // shuffles, then add the totals of the waves before them (a serial scan
@@ -1366,7 +1366,7 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, 
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nt; i += 1024) {
-        const uint32_t t = group + i * groups;
+        const uint32_t t = pt_tile_group_tile(tiles, groups, group, i);
         order[start + atomicAdd(&count[key(t)], 1u)] = t;
     }
 }

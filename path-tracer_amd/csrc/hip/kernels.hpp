@@ -141,11 +141,23 @@ hipError_t pt_launch_vertex_decode(const uint2* v, uint32_t n, float4* attr, flo
 // (pt_tile_group_count of them) and the dispatch-order segment starting at
 // pt_tile_group_start.  pt_launch_tile_order sorts one group's segment
 // longest-first (groups = 1: the whole frame).
-inline uint32_t pt_tile_group_count(uint32_t tiles, uint32_t groups, uint32_t group)
+#ifndef PT_SPLIT_CONTIG
+#define PT_SPLIT_CONTIG 0   // experiment builds: 1 = group g owns the g-th contiguous run of tiles
+#endif
+__host__ __device__ inline uint32_t pt_tile_group_count(uint32_t tiles, uint32_t groups, uint32_t group)
 {
+    if (PT_SPLIT_CONTIG) {
+        const uint32_t chunk = (tiles + groups - 1) / groups, first = group * chunk;
+        return first < tiles ? (tiles - first < chunk ? tiles - first : chunk) : 0u;
+    }
     return group < tiles ? (tiles - group + groups - 1) / groups : 0u;
 }
-inline uint32_t pt_tile_group_start(uint32_t tiles, uint32_t groups, uint32_t group)
+// The i-th tile of a group.
+__host__ __device__ inline uint32_t pt_tile_group_tile(uint32_t tiles, uint32_t groups, uint32_t group, uint32_t i)
+{
+    return PT_SPLIT_CONTIG ? group * ((tiles + groups - 1) / groups) + i : group + i * groups;
+}
+__host__ __device__ inline uint32_t pt_tile_group_start(uint32_t tiles, uint32_t groups, uint32_t group)
 {
     uint32_t s = 0;
     for (uint32_t h = 0; h < group; h++) s += pt_tile_group_count(tiles, groups, h);

@@ -1300,7 +1300,7 @@ static int EnsureOrderGroups(pt_device* d, pt_basic_renderer* r, uint32_t K)
     std::vector<uint32_t> order(T);
     uint32_t i = 0;
     for (uint32_t g = 0; g < K; g++)
-        for (uint32_t t = g; t < T; t += K) order[i++] = t;
+        for (uint32_t j = 0; j < pt_tile_group_count(T, K, g); j++) order[i++] = pt_tile_group_tile(T, K, g, j);
     PT_WAIT(d);
     PT_HIP(hipMemcpy(r->order.ptr, order.data(), (size_t)T * 4, hipMemcpyHostToDevice));
     r->order_groups = K;
@@ -1311,7 +1311,17 @@ static int EnsureGroupStreams(pt_device* d, uint32_t K)
 {
     if (!d->fork_event) PT_HIP(hipEventCreateWithFlags(&d->fork_event, hipEventDisableTiming));
     for (uint32_t g = 0; g + 1 < K; g++) {
+#if PT_SPLIT_PRIO
+        // Experiment builds: group streams at the lowest (1) or highest (2) priority.
+        if (!d->group_stream[g]) {
+            int least = 0, greatest = 0;
+            PT_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            PT_HIP(hipStreamCreateWithPriority(&d->group_stream[g], hipStreamNonBlocking,
+                                               PT_SPLIT_PRIO == 1 ? least : greatest));
+        }
+#else
         if (!d->group_stream[g]) PT_HIP(hipStreamCreateWithFlags(&d->group_stream[g], hipStreamNonBlocking));
+#endif
         if (!d->join_event[g]) PT_HIP(hipEventCreateWithFlags(&d->join_event[g], hipEventDisableTiming));
     }
     return 0;
