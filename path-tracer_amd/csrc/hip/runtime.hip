@@ -972,7 +972,10 @@ int ptReadResolvedImageSRGB8(pt_device* d, pt_sample_buffer* b, uint8_t* rgba8)
 // Rounds between two longest-first tile-order sorts (C3 / C5 / C2 at 4:
 // +3.4 / +4.9 / -1.4 %, at 16: +3.9 / +5.3 / 0 % vs natural order; period 1
 // C3 -2.4 %: DESIGN.md §4).
-constexpr uint32_t TILE_ORDER_PERIOD = 16;
+#ifndef PT_TILE_ORDER_PERIOD
+#define PT_TILE_ORDER_PERIOD 16   // experiment builds may change it
+#endif
+constexpr uint32_t TILE_ORDER_PERIOD = PT_TILE_ORDER_PERIOD;
 
 pt_basic_renderer* ptCreateBasicRendererStreams(pt_device* d, pt_scene* s, pt_sample_buffer* b, uint32_t rank,
                                                 uint32_t nranks, uint32_t streams)
