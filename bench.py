@@ -91,6 +91,57 @@ def cpu_model():
     return None
 
 
+def pick_cores(n, sample_s=0.25):
+    """n logical CPUs of this process's affinity mask on n distinct physical
+    cores of one package, the least busy over a /proc/stat sample (the host
+    is shared with other GPUs' jobs), and a description; (None, reason) when
+    the topology is unreadable or too small.  Unpinned, the oracle's threads
+    (created per round) land across both packages and ran 5.9-7.1 Mrays/s
+    against 9.9-11.3 pinned to 16 distinct cores (tools/cpu_affinity.py,
+    profiles/r05_aff): the placement, not the host's load, made round 4's
+    and round 5's two clusters."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+        topo = {}
+        for c in cpus:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            topo[c] = (int(open(base + "physical_package_id").read()), int(open(base + "core_id").read()))
+
+        def stat():
+            out = {}
+            for line in open("/proc/stat"):
+                f = line.split()
+                if f[0].startswith("cpu") and f[0] != "cpu":
+                    v = [int(x) for x in f[1:]]
+                    out[int(f[0][3:])] = (sum(v), v[3] + (v[4] if len(v) > 4 else 0))
+            return out
+        a = stat()
+        time.sleep(sample_s)
+        b = stat()
+    except (OSError, ValueError, AttributeError, KeyError):
+        return None, "topology unreadable: threads unpinned"
+
+    def busy(c):
+        dt = b[c][0] - a[c][0]
+        return 1.0 - (b[c][1] - a[c][1]) / dt if dt > 0 else 1.0
+    cores = {}
+    for c in cpus:
+        cores.setdefault(topo[c], []).append(c)
+    # A core's load: its busiest sibling; its CPU: its least busy sibling.
+    load = {k: max(busy(c) for c in v) for k, v in cores.items()}
+    best = None
+    for pkg in sorted({k[0] for k in cores}):
+        ks = sorted((k for k in cores if k[0] == pkg), key=lambda k: load[k])[:n]
+        if len(ks) == n and (best is None or sum(load[k] for k in ks) < best[0]):
+            best = (sum(load[k] for k in ks), pkg, ks)
+    if best is None:
+        return None, f"fewer than {n} physical cores in one package: threads unpinned"
+    _, pkg, ks = best
+    chosen = sorted(min(cores[k], key=busy) for k in ks)
+    return set(chosen), (f"{n} threads pinned to {n} distinct physical cores of package {pkg}, the least busy "
+                         f"over a {sample_s} s /proc/stat sample (mean busy {best[0] / n:.2f})")
+
+
 def cpu_baseline(pt, scene, width, height, config, settle_rounds=34, min_rounds=32, max_seconds=30.0):
     """Time the CPU oracle (scalar C++ restatement, std::thread over host
     cores) on the same scene and frame.  Bounded: Reset + Run(2) and
@@ -111,25 +162,34 @@ def cpu_baseline(pt, scene, width, height, config, settle_rounds=34, min_rounds=
         allowed = host_cpus
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     threads = max(1, min(allowed, omp) if omp > 0 else allowed)
+    # The oracle's worker threads are created per round and inherit this
+    # thread's mask: pin it to `threads` distinct cores for the measurement.
+    home = os.sched_getaffinity(0)
+    pinned, placement = pick_cores(threads) if threads < allowed else (None, "every affinity CPU, unpinned")
     o = oracle_lib.OracleRenderer(scene.packs(), width, height, threads=threads)
-    o.RenderFlags = 3
-    o.reset()
-    o.run(2)
-    for _ in range(settle_rounds):
-        o.run(1)
-    r0, s0 = o.counters()
-    t0 = time.perf_counter()
-    c0 = time.process_time()
-    rounds = 0
-    while rounds < min_rounds or time.perf_counter() - t0 < max_seconds / 2:
-        o.run(1)
-        rounds += 1
-        if time.perf_counter() - t0 > max_seconds:
-            break
-    dt = time.perf_counter() - t0
-    cpu_s = time.process_time() - c0
-    r1, s1 = o.counters()
-    o.close()
+    try:
+        if pinned:
+            os.sched_setaffinity(0, pinned)
+        o.RenderFlags = 3
+        o.reset()
+        o.run(2)
+        for _ in range(settle_rounds):
+            o.run(1)
+        r0, s0 = o.counters()
+        t0 = time.perf_counter()
+        c0 = time.process_time()
+        rounds = 0
+        while rounds < min_rounds or time.perf_counter() - t0 < max_seconds / 2:
+            o.run(1)
+            rounds += 1
+            if time.perf_counter() - t0 > max_seconds:
+                break
+        dt = time.perf_counter() - t0
+        cpu_s = time.process_time() - c0
+        r1, s1 = o.counters()
+    finally:
+        os.sched_setaffinity(0, home)
+        o.close()
     share = "the job's CPU share (OMP_NUM_THREADS)" if omp > 0 and omp < allowed else "every affinity CPU"
     return {
         "value": round((r1 - r0) / dt / 1e6, 4),
@@ -140,15 +200,15 @@ def cpu_baseline(pt, scene, width, height, config, settle_rounds=34, min_rounds=
         "host_cpus": host_cpus,
         "affinity_cpus": allowed,
         "omp_num_threads": omp or None,
+        "placement": placement,
+        "pinned_cpus": sorted(pinned) if pinned else None,
         "cpu_model": cpu_model(),
         "kind": "port",
         "sample": f"C{config} {width}x{height}, {rounds} consecutive rounds after Reset + Run(2) + "
                   f"{settle_rounds} settle rounds ({(r1 - r0)} rays, {(s1 - s0)} samples, {dt:.1f} s timed)",
         "msamples_per_s": round((s1 - s0) / dt / 1e6, 4),
-        # The host is shared with the other GPUs' jobs: the wall-clock rate
-        # moves +-40 % between runs minutes apart.  CPU seconds
-        # the process's threads actually ran give the rate on `threads`
-        # dedicated cores, which moves less.
+        # CPU seconds the process's threads actually ran (= threads x wall
+        # time when the pinned cores were not shared).
         "cpu_seconds": round(cpu_s, 2),
         "mrays_per_cpu_s_x_threads": round((r1 - r0) / max(cpu_s, 1e-9) * threads / 1e6, 4),
     }

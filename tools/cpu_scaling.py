@@ -6,7 +6,9 @@ the per-round cost is stationary), then each thread count times `rounds`
 consecutive rounds of the same render (oracle_set_threads between them).
 
 VERDICT r04 #6: round 4 timed 2 rounds right after Reset (the shortest paths)
-per thread count.  On the GPU box a job's CPU share is 16 threads
+per thread count.  Each thread count runs pinned to that many distinct
+physical cores of one package (bench.pick_cores), as bench.py's cpu_baseline
+does.  On the GPU box a job's CPU share is 16 threads
 (OMP_NUM_THREADS) of a 256-CPU host shared with the other GPUs' jobs; this
 tool stays inside that share, and states the all-core figure as an
 extrapolation of the measured per-thread rate, not a measurement.
@@ -52,8 +54,14 @@ def main():
     settle_s = time.perf_counter() - t0
     print(json.dumps({"settle_rounds": a.settle, "settle_s": round(settle_s, 2), "threads": max(counts)}), flush=True)
     rows = []
+    home = os.sched_getaffinity(0)
+    allowed = len(home)
     for t in counts:
         o.set_threads(t)
+        # The same placement as bench.py's cpu_baseline: t threads pinned to
+        # t distinct, least busy physical cores of one package.
+        pinned, placement = bench.pick_cores(t) if t < allowed else (None, "every affinity CPU, unpinned")
+        os.sched_setaffinity(0, pinned if pinned else home)
         r0, s0 = o.counters()
         t0 = time.perf_counter()
         c0 = time.process_time()
@@ -72,7 +80,9 @@ def main():
                "median_round_s": round(per_round[len(per_round) // 2], 4),
                "min_round_s": round(per_round[0], 4), "max_round_s": round(per_round[-1], 4),
                "cpu_seconds": round(cpu_s, 2),
-               "mrays_per_cpu_s_x_threads": round((r1 - r0) / max(cpu_s, 1e-9) * t / 1e6, 4)}
+               "mrays_per_cpu_s_x_threads": round((r1 - r0) / max(cpu_s, 1e-9) * t / 1e6, 4),
+               "placement": placement, "pinned_cpus": sorted(pinned) if pinned else None}
+        os.sched_setaffinity(0, home)
         rows.append(row)
         print(json.dumps(row), flush=True)
     o.close()
