@@ -493,6 +493,14 @@ def main():
     # frames are mostly round batches, with two single fused rounds each).
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"] * kernels[k]["rounds"])
     achieved = kernels[dom]["gbps"]
+    wall_round_ms = dt / max(rounds_local, 1) * 1e3
+    ksum = {k: v["avg_ms"] * (split["groups"] if k in ("extend", "shade") else 1) for k, v in kernels.items()
+            if k in ("extend", "shade", "round", "rounds")}
+    share_ms = wall_round_ms * ksum[dom] / max(sum(ksum.values()), 1e-12) if dom in ksum else None
+    apportioned = ({"ms_per_round": round(share_ms, 4), "wall_ms_per_round": round(wall_round_ms, 4),
+                    "achieved": round(ALG_BYTES[dom] * slots_owned / (share_ms * 1e-3) / 1e9, 2),
+                    "frac": round(ALG_BYTES[dom] * slots_owned / (share_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5)}
+                   if share_ms else None)
     # The committed PMC profile of this workload: the whole frame's launches
     # (N = 1 and sample shards), or rank 0's band partition with its path
     # streams (a launch over other slots than the whole frame's).
@@ -598,6 +606,12 @@ def main():
             # its own duration (path_frac is the whole frame's).
             "split_groups": split["groups"],
             "slots_per_timed_launch": round(launch_slots),
+            # The frame's wall time per round shared among the kernels in
+            # proportion to their summed launch time per round (groups x a
+            # group's launch): with tile groups the launches overlap, so this
+            # is the dominant kernel's share of the chip, comparable with an
+            # unsplit launch's time.
+            "apportioned": apportioned,
             "alg_bytes_per_slot": ALG_BYTES[dom],
             "launch_avg_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
             "launches_timed": {**{k: v[0] for k, v in kstats.items()}, "every_nth_round": args.profile_period},
