@@ -90,11 +90,25 @@ def intersect_bounding_box(origin, velocity, reach, mn, mx):
     return float(lib().oracle_intersect_bounding_box(p[0], p[1], float(reach), p[2], p[3]))
 
 
+def default_threads():
+    import os
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(allowed, omp) if omp > 0 else allowed)
+
+
 class OracleRenderer:
     """Per-pixel CPU restatement of basic_trace + basic_scatter."""
 
     def __init__(self, packs, width, height, rank=0, nranks=1, threads=0):
+        """threads: 0 = the job's CPU share (OMP_NUM_THREADS when set, as on
+        the GPU box, else this process's affinity CPUs), not every host CPU."""
         from path_tracer_amd import _native as N  # noqa: F401  (packs struct type)
+        if threads <= 0:
+            threads = default_threads()
         self._h = lib().oracle_create(C.addressof(packs), width, height, rank, nranks, threads)
         if not self._h:
             raise RuntimeError("oracle_create failed")

@@ -7,7 +7,7 @@ pixel compared with the CPU oracle bit for bit.  Prints one JSON line.
 A random scene of tests/fuzz_scenes.py runs as CONFIG "fuzz:SEED" at
 320x240 with the seed's RenderFlags, roulette and camera.
 
-usage: python tools/long_parity.py [CONFIG | fuzz:SEED] [ROUNDS] [CAMERA]"""
+usage: python tools/long_parity.py [CONFIG | fuzz:SEED] [ROUNDS] [CAMERA] [--batched]"""
 import json
 import sys
 import time
@@ -23,6 +23,12 @@ import oracle_lib  # noqa: E402
 
 
 def main():
+    # --batched: the GPU side runs its Run(1) rounds through
+    # ptRunBasicRendererRounds in chunks of 50 (tile groups on concurrent
+    # streams on full frames); the oracle runs the same rounds one by one.
+    batched = "--batched" in sys.argv
+    if batched:
+        sys.argv.remove("--batched")
     pt = load()
     cfg = sys.argv[1] if len(sys.argv) > 1 else "3"
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 64
@@ -50,18 +56,27 @@ def main():
         x.CameraIndex = camera
         x.reset()
         x.run(2)
-    for i in range(rounds - 2):
-        r.run(1)
-        o.run(1)
-        if i % 50 == 49:   # progress (the oracle takes ~0.3 s a round at C3)
-            print(f"round {i + 3} of {rounds}, {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+    done = 0
+    while done < rounds - 2:
+        n = min(50, rounds - 2 - done)
+        if batched:
+            r.run_rounds(n)
+        else:
+            for _ in range(n):
+                r.run(1)
+        for _ in range(n):
+            o.run(1)
+        done += n
+        # progress (the oracle takes ~0.3 s a round at C3)
+        print(f"round {done + 2} of {rounds}, {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
     dev.synchronize()
     g, want = r.read_state(), o.state()
     bad = {}
     for f in ("origin", "packed_velocity", "lambda0", "throughput", "probability", "sample", "active01", "active23"):
         bad[f] = int(np.sum(np.any((g[f].view(np.uint32) != want[f].view(np.uint32)).reshape(H, W, -1), axis=-1)))
     acc_bad = int(np.sum(np.any(sb.read().view(np.uint32) != o.accum().view(np.uint32), axis=-1)))
-    print(json.dumps({"config": cfg, "camera": camera, "size": [W, H], "rounds": rounds, "state_mismatch_px": bad,
+    print(json.dumps({"config": cfg, "camera": camera, "size": [W, H], "rounds": rounds, "batched": batched,
+                      "split": r.split() if batched else None, "state_mismatch_px": bad,
                       "accum_mismatch_px": acc_bad, "samples": float(o.accum()[..., 3].sum()),
                       "seconds": round(time.time() - t0, 1)}), flush=True)
 
