@@ -9,6 +9,7 @@ A random scene of tests/fuzz_scenes.py runs as CONFIG "fuzz:SEED" at
 
 usage: python tools/long_parity.py [CONFIG | fuzz:SEED] [ROUNDS] [CAMERA] [--batched]"""
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -48,7 +49,16 @@ def main():
     ds.update(s)
     sb = pt.SampleBuffer(dev, W, H)
     r = pt.BasicRenderer(dev, ds, sb)
-    o = oracle_lib.OracleRenderer(s.packs(), W, H)
+    # The oracle's per-round threads run on this process's share of distinct
+    # physical cores of one package (bench.pick_cores; unpinned they spread
+    # over both NUMA packages and run ~1.6x slower).
+    sys.path.insert(0, str(ROOT))
+    import bench
+    threads = oracle_lib.default_threads()
+    pinned, _ = bench.pick_cores(threads) if threads < len(os.sched_getaffinity(0)) else (None, None)
+    if pinned:
+        os.sched_setaffinity(0, pinned)
+    o = oracle_lib.OracleRenderer(s.packs(), W, H, threads=threads)
     t0 = time.time()
     for x in (r, o):
         x.RenderFlags = flags
