@@ -167,3 +167,69 @@ def test_split_profiling_times_group_zero(pt, dev):
     r.close()
     sb.close()
     ds.close()
+
+
+def test_split_band_partition_with_path_streams(pt, dev):
+    """A band partition (rank 1 of 3) carrying two path streams per pixel:
+    every stream's state and own accumulator equal under three tile groups
+    and unsplit."""
+    s = scene_for(pt, 3)
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    W, H = 320, 180
+    out = []
+    for k in (1, 3):
+        sb = pt.SampleBuffer(dev, W, H)
+        r = pt.BasicRenderer(dev, ds, sb, rank=1, nranks=3, streams=2)
+        r.RenderFlags = 3
+        r.set_fused_rounds(0)
+        r.set_split(k)
+        r.reset()
+        r.run(2)
+        r.run_rounds(9)
+        r.merge_streams()
+        dev.synchronize()
+        out.append(([r.read_state(j) for j in range(2)], [r.read_accumulator(j) for j in range(2)], sb.read()))
+        r.close()
+        sb.close()
+    (sa, aa, ma), (sb2, ab, mb) = out
+    for j in range(2):
+        compare_state(sa[j], sb2[j])
+        assert np.array_equal(bits(aa[j]), bits(ab[j])), f"stream {j} accumulator differs"
+    assert np.array_equal(bits(ma), bits(mb))
+    ds.close()
+
+
+def test_split_after_resume(pt, dev):
+    """Resume into a new renderer (state, accumulator, FrameIndex), then
+    rounds in three tile groups: equal to the uninterrupted unsplit render."""
+    s = scene_for(pt, 2)
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    W, H = 128, 128
+    ref = render(pt, dev, ds, W, H, [1, 1], [4, 6])
+    sb = pt.SampleBuffer(dev, W, H)
+    a = pt.BasicRenderer(dev, ds, sb)
+    a.RenderFlags = 3
+    a.set_fused_rounds(0)
+    a.reset()
+    a.run(2)
+    a.run_rounds(4)
+    saved, acc, frame = a.read_state(), sb.read(), a.FrameIndex
+    a.close()
+    sb.close()
+    sb = pt.SampleBuffer(dev, W, H)
+    b = pt.BasicRenderer(dev, ds, sb)
+    b.RenderFlags = 3
+    b.set_fused_rounds(0)
+    b.set_split(3)
+    sb.write(acc)
+    b.FrameIndex = frame
+    b.write_state(saved)
+    b.run_rounds(6)
+    dev.synchronize()
+    compare_state(b.read_state(), ref[0])
+    assert np.array_equal(bits(sb.read()), bits(ref[1]))
+    b.close()
+    sb.close()
+    ds.close()
