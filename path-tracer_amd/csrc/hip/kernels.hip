@@ -1290,6 +1290,9 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
 {
     __shared__ E smem[CAP * 256];
     __shared__ float4 ncache[NC ? 4 * PT_NODE_CACHE_PAIRS : 1];
+    if constexpr (kRendererSource<Src>) {
+        if (src.L.stop && *src.L.stop) return;   // a guarded round past the frame's target
+    }
     const uint32_t ncn = NC ? NodeCacheFill(S, ncache) : 0u;
     // Tile order: the slot renderer dispatches the tiles whose waves took
     // longest in the previous round first (tile_order_kernel), so the
@@ -1368,6 +1371,31 @@ __global__ __launch_bounds__(1024) void tile_order_kernel(const uint32_t* cost, 
     for (uint32_t i = threadIdx.x; i < nt; i += 1024) {
         const uint32_t t = pt_tile_group_tile(tiles, groups, group, i);
         order[start + atomicAdd(&count[key(t)], 1u)] = t;
+    }
+}
+
+// Guarded rounds (ptRenderFrame's last rounds, enqueued without a read-back
+// between them): before each, the paths completed since the Reset -- the sum
+// of the per-wave done words, as ptGetStats adds them -- against the frame's
+// target.  Reached: flags[0] = 1, and this and every later launch of the
+// frame returns at once (dslots.stop); else the round runs and flags[1]
+// counts it.  So the frame still ends at the first round whose total reaches
+// the target.
+__global__ __launch_bounds__(1024) void guard_kernel(const uint32_t* done, uint32_t words, unsigned long long target,
+                                                     uint32_t* flags)
+{
+    __shared__ unsigned long long part[1024];
+    unsigned long long s = 0;
+    for (uint32_t i = threadIdx.x; i < words; i += 1024) s += done[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (uint32_t h = 512; h > 0; h >>= 1) {
+        if (threadIdx.x < h) part[threadIdx.x] += part[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && flags[0] == 0u) {
+        if (part[0] >= target) flags[0] = 1u;
+        else flags[1] += 1u;
     }
 }
 
@@ -1768,6 +1796,7 @@ __global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void shade_kernel(dscen
 {
     // Tiles in extend's longest-first order too: tiles with long traversals
     // also shade more hits (C5 shade -3 %).
+    if (L.stop && *L.stop) return;   // a guarded round past the frame's target
     ShadeStatsBegin();
     ShadeTile<MATS, COMPACT>(S, L, F, Pm, L.order ? L.order[blockIdx.x] : blockIdx.x);
     ShadeStatsEnd();
@@ -1933,6 +1962,7 @@ __global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void round_kernel(
     dscene S, dslots L, dframe F, dparams Pm)
 {
     __shared__ E smem[CAP * 256];
+    if (L.stop && *L.stop) return;   // a guarded round past the frame's target
     const uint32_t tile = L.order ? L.order[blockIdx.x] : blockIdx.x;
     ExtendTile<ray_source_slots, false, CAP, E>(S, ray_source_slots{L, F}, L.n, nullptr, 0, smem, tile,
                                                  L.order != nullptr);
@@ -2118,6 +2148,12 @@ hipError_t pt_launch_vertex_decode(const uint2* v, uint32_t n, float4* attr, flo
 {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(ptd::vertex_decode_kernel, dim3((n + 255) / 256), dim3(256), 0, st, v, n, attr, vv);
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_guard(const uint32_t* done, uint32_t words, uint64_t target, uint32_t* flags, hipStream_t st)
+{
+    hipLaunchKernelGGL(ptd::guard_kernel, dim3(1), dim3(1024), 0, st, done, words, (unsigned long long)target, flags);
     return hipGetLastError();
 }
 

@@ -33,6 +33,7 @@ struct dslots {
     uint32_t* order;    // extend's block -> tile map (longest previous extend first), or null
     uint32_t* done;     // per wave of 64 slots: paths completed by shade since the last Reset (ptGetStats)
     uint32_t* spill;    // traversal stack spill: (needed - LDS capacity) rows x n
+    const uint32_t* stop = nullptr;   // guarded rounds (ptRenderFrame's last rounds): set -> the launch returns
     uint32_t n;
     uint32_t tile_count;    // n / 256: one block per tile
 #if PT_EXP_CLASSQ
@@ -164,6 +165,10 @@ __host__ __device__ inline uint32_t pt_tile_group_start(uint32_t tiles, uint32_t
     return s;
 }
 hipError_t pt_launch_tile_order(const ptd::dslots& L, hipStream_t st, uint32_t groups = 1, uint32_t group = 0);
+// Guarded rounds (ptRenderFrame): flags[0] := 1 once the done words' sum (the
+// paths completed since the Reset, ptGetStats) reaches target; while it is
+// 0, flags[1] counts the rounds that run.
+hipError_t pt_launch_guard(const uint32_t* done, uint32_t words, uint64_t target, uint32_t* flags, hipStream_t st);
 // Fused round (extend + shade per tile in one launch, round_kernel): the
 // tiles the GPU can hold at once for this scene (0: not available), and the
 // launch (hipErrorNotSupported when the scene needs a spilled stack).

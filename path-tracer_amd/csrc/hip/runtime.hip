@@ -190,6 +190,7 @@ struct pt_basic_renderer {
     int openpbr = 0;                    // shade OpenPBR materials (ptSetBasicRendererOpenPBR)
     uint32_t round_batch = 0;           // rounds per launch of consecutive Run(1) rounds (0: automatic)
     uint32_t split = 0;                 // tile groups of consecutive rounds (ptSetBasicRendererSplit): 0 auto, 1 off
+    dbuf<uint32_t> guard;               // guarded rounds' {stop, rounds run} (ptRenderFrame)
     uint32_t order_groups = 1;          // the group structure the order array holds (tile_order_kernel)
     uint64_t pixels = 0;                // image pixels owned
     uint32_t streams = 1;               // path streams per owned pixel (ptCreateBasicRendererStreams)
@@ -1107,6 +1108,7 @@ void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
     r->tilecost.release(); r->order.release();
     r->done.release();
     r->spill.release();
+    r->guard.release();
     r->accx.release();
     delete r;
 }
@@ -1504,6 +1506,50 @@ int ptGetStats(pt_device* d, pt_basic_renderer* r, uint64_t* rays, uint64_t* sam
     return 0;
 }
 
+// n guarded Run(1) rounds (FrameIndex + 1 ... + n) on the device stream:
+// each preceded by guard_kernel, the launches of a round past the target
+// returning at once.  Returns the rounds that ran in *ran and leaves
+// FrameIndex and the ray count as those rounds left them.
+static int RunGuardedRounds(pt_device* d, pt_basic_renderer* r, uint32_t n, uint64_t target, uint32_t* ran)
+{
+    PT_HIP(hipSetDevice(d->id));
+    if (int e = EnsureSpill(r)) return e;
+    if (int e = SyncRecordForm(d, r)) return e;
+    if (!r->guard.ptr) PT_HIP(r->guard.alloc(2));
+    PT_HIP(hipMemsetAsync(r->guard.ptr, 0, 2 * sizeof(uint32_t), d->stream));
+    ptd::dslots L = r->slots;
+    L.stop = r->guard.ptr;
+    const ptd::dframe F = Frame(r);
+    const bool fused = RoundFused(r, L);
+    const uint32_t mats = ShadeMats(r);
+    const bool compact = ShadeCompact(r);
+    const uint64_t base = r->params.FrameIndex;
+    for (uint32_t i = 0; i < n; i++) {
+        PT_HIP(pt_launch_guard(r->done.ptr, r->slots.n / 64 + 1, target, r->guard.ptr, d->stream));
+        const ptd::dparams P = Params(r, base + i + 1);
+        if (fused) {
+            PT_HIP(pt_launch_round(r->scene->d, L, F, P, mats, d->stream));
+        } else {
+            PT_HIP(pt_launch_extend(r->scene->d, L, F, L.spill, d->stream));
+            PT_HIP(pt_launch_shade(r->scene->d, L, F, P, mats, compact, d->stream));
+        }
+    }
+    uint32_t flags[2] = {0, 0};
+    PT_WAIT(d);
+    PT_HIP(hipMemcpy(flags, r->guard.ptr, sizeof(flags), hipMemcpyDeviceToHost));
+    *ran = flags[1];
+    r->params.FrameIndex = base + flags[1];
+    r->rays += r->valid_slots * flags[1];
+    d->run_tick += flags[1];
+    r->order_tick += flags[1];
+    return 0;
+}
+
+constexpr double GUARD_PREDICTED = 8.0;   // rounds left, by the last batch's rate, for the guarded end
+#ifndef PT_FRAME_GUARD
+#define PT_FRAME_GUARD 1   // A/B builds: 0 = round 4's read-back after every batch
+#endif
+
 // Benchmark-mode frame: Reset, Run(2) as after a restart
 // (application.cpp:109-110), then Run(1) rounds -- one new seed each, as the
 // application's frame loop issues them (application.cpp:100-115,
@@ -1513,7 +1559,10 @@ int ptGetStats(pt_device* d, pt_basic_renderer* r, uint64_t* rays, uint64_t* sam
 // never longer than the rounds that could not reach the target even if every
 // slot completed a path each round, or than 90 % of the rounds the last
 // batch's completion rate predicts, and within the last 16 predicted rounds
-// only the former.  So the frame ends at the reference's round (the first
+// only the former.  The first batch after Run(2) needs no read-back (at most
+// 2 px paths completed so far), and the last rounds (at most GUARD_PREDICTED
+// by the rate) run guarded: a device-side check before each round stops the
+// rest once the target is reached, so they need one read-back in all.  So the frame ends at the reference's round (the first
 // whose total reaches the target) unless the completion rate rises by more
 // than 1/0.9 - 1 = 11 % within one rate-sized batch; the rate of a frame
 // past its first rounds moves by well under 1 % per batch (the C3 1024-spp
@@ -1529,6 +1578,17 @@ int ptRenderFrame(pt_device* d, pt_basic_renderer* r, uint64_t target_samples, u
     uint64_t samples = 0, prev = 0;
     uint32_t last_batch = 0;
     const uint64_t px = std::max<uint64_t>(r->valid_slots, 1);   // paths one round can complete
+    // Every round completes at most px paths, so the two rounds of Run(2)
+    // leave at least target - 2 px to go: that many rounds' worth runs
+    // before the first read-back.
+    if (PT_FRAME_GUARD && target_samples > 2 * px) {
+        const uint64_t k = std::min<uint64_t>((target_samples - 2 * px + px - 1) / px, max_rounds - rounds);
+        if (k >= 1) {
+            if (int e = RunRounds(d, r, k)) return e;
+            rounds += (uint32_t)k;
+            last_batch = rounds;   // the rate below: completions since the Reset per round
+        }
+    }
     for (;;) {
         if (int e = ptGetStats(d, r, nullptr, &samples)) return e;
         if (samples >= target_samples || rounds >= max_rounds) break;
@@ -1540,8 +1600,23 @@ int ptRenderFrame(pt_device* d, pt_basic_renderer* r, uint64_t target_samples, u
             // last 16 predicted rounds only the rounds that cannot overshoot,
             // so a rate that rises near the end cannot carry the frame past
             // the round that first reaches the target.
-            const uint64_t kr = (uint64_t)(0.9 * (double)remaining / rate);
+            const double predicted = (double)remaining / rate;
+            const uint64_t kr = (uint64_t)(0.9 * predicted);
             if (kr >= 16) k = std::max<uint64_t>(k, kr);
+            // The last few rounds: guarded, enqueued together with one
+            // read-back after them instead of one per batch (C1's 24-round
+            // frame took five read-backs).
+            if (PT_FRAME_GUARD && predicted <= GUARD_PREDICTED) {
+                const uint32_t n = (uint32_t)std::min<uint64_t>((uint64_t)(1.25 * predicted) + 2, max_rounds - rounds);
+                if (n >= 2) {
+                    uint32_t ran = 0;
+                    if (int e = RunGuardedRounds(d, r, n, target_samples, &ran)) return e;
+                    rounds += ran;
+                    prev = samples;
+                    last_batch = ran;
+                    continue;
+                }
+            }
         }
         k = std::max<uint64_t>(1, std::min<uint64_t>(k, max_rounds - rounds));
         if (int e = RunRounds(d, r, k)) return e;
