@@ -1356,6 +1356,11 @@ static int RunRoundsSplit(pt_device* d, pt_basic_renderer* r, uint64_t k, uint32
     }
     PT_HIP(hipEventRecord(d->fork_event, d->stream));
     for (uint32_t g = 1; g < K; g++) PT_HIP(hipStreamWaitEvent(S[g], d->fork_event, 0));
+#if PT_SPLIT_STAGGER
+    static hipEvent_t stagger[PT_MAX_SPLIT - 1] = {};
+    for (uint32_t g = 0; g + 1 < K; g++)
+        if (!stagger[g]) PT_HIP(hipEventCreateWithFlags(&stagger[g], hipEventDisableTiming));
+#endif
     auto rounds = [&]() -> int {
         for (uint64_t i = 0; i < k; i++) {
             r->params.FrameIndex += 1;
@@ -1366,7 +1371,15 @@ static int RunRoundsSplit(pt_device* d, pt_basic_renderer* r, uint64_t k, uint32
                 event_pair ep{};
                 if (g == 0)
                     if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled)) return e;
+#if PT_SPLIT_STAGGER
+                // Experiment builds: group g's first extend starts after group
+                // g - 1's (the groups begin the batch a launch apart).
+                if (i == 0 && g > 0) PT_HIP(hipStreamWaitEvent(S[g], stagger[g - 1], 0));
+#endif
                 PT_HIP(pt_launch_extend(r->scene->d, G[g], F, r->slots.spill, S[g]));
+#if PT_SPLIT_STAGGER
+                if (i == 0 && g + 1 < K) PT_HIP(hipEventRecord(stagger[g], S[g]));
+#endif
                 if (g == 0) {
                     if (int e = EndTimed(d, ep)) return e;
                     if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled)) return e;
