@@ -7,7 +7,7 @@ pixel compared with the CPU oracle bit for bit.  Prints one JSON line.
 A random scene of tests/fuzz_scenes.py runs as CONFIG "fuzz:SEED" at
 320x240 with the seed's RenderFlags, roulette and camera.
 
-usage: python tools/long_parity.py [CONFIG | fuzz:SEED] [ROUNDS] [CAMERA] [--batched]"""
+usage: python tools/long_parity.py [CONFIG | fuzz:SEED] [ROUNDS] [CAMERA] [--batched] [--split K]"""
 import json
 import os
 import sys
@@ -30,6 +30,11 @@ def main():
     batched = "--batched" in sys.argv
     if batched:
         sys.argv.remove("--batched")
+    split = 0   # --split K: force K tile groups (0: automatic)
+    if "--split" in sys.argv:
+        i = sys.argv.index("--split")
+        split = int(sys.argv[i + 1])
+        del sys.argv[i:i + 2]
     pt = load()
     cfg = sys.argv[1] if len(sys.argv) > 1 else "3"
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 64
@@ -49,6 +54,9 @@ def main():
     ds.update(s)
     sb = pt.SampleBuffer(dev, W, H)
     r = pt.BasicRenderer(dev, ds, sb)
+    r.set_split(split)
+    if split > 1:
+        r.set_fused_rounds(0)   # forced groups: the small frames' rounds would otherwise run fused
     # The oracle's per-round threads run on this process's share of distinct
     # physical cores of one package (bench.pick_cores; unpinned they spread
     # over both NUMA packages and run ~1.6x slower).
