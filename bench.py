@@ -271,6 +271,8 @@ def main():
                     help="N-rank launch plumbing only (gloo, no GPU): CPU test of the launcher")
     ap.add_argument("--split", type=int, default=0,
                     help="tile groups on concurrent streams (ptSetBasicRendererSplit): 0 automatic, 1 off, K")
+    ap.add_argument("--class-lists", type=int, default=0,
+                    help="class-pure shade in tile groups (ptSetBasicRendererClassLists): 0 automatic, 1 off")
     ap.add_argument("--streams", type=int, default=0,
                     help="path streams per owned pixel (0: auto -- bands fill ~2^21 slots per launch, samples 1)")
     ap.add_argument("--inject-failure", type=int, default=-1, metavar="RANK",
@@ -334,6 +336,11 @@ def main():
     # Tile groups on concurrent streams (ptSetBasicRendererSplit): profiling
     # times group 0's launches, which cover timed_tiles of the tiles.
     r.set_split(args.split)
+    try:
+        r.set_class_lists(args.class_lists)
+        class_lists = r.class_lists()
+    except AttributeError:   # an older library under PT_HIP_LIB (A/B builds)
+        class_lists = None
     split = r.split()
     launch_slots = slots_owned * split["timed_tiles"] / max(split["tiles"], 1) if split["groups"] > 1 else slots_owned
     # This rank's frame target (Σ alpha): samples -> 1/N of spp x frame,
@@ -571,6 +578,7 @@ def main():
             "streams": streams,
             "slots_per_launch_rank0": slots_owned,
             "split": split["groups"],
+            "class_lists": class_lists,
             "frame_target_samples_rank0": target,
             "mesh_faces": info.mesh_face_count,
             "image_identity": identity,

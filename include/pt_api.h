@@ -256,6 +256,15 @@ int                ptSetBasicRendererRoundBatch(pt_basic_renderer* renderer, uin
  * tiles of group 0 (the launches kernel profiling times) and all tiles; any
  * pointer may be NULL.  Default 0. */
 #define PT_MAX_SPLIT 4
+/* Class-pure shade inside tile groups (no reference counterpart: a launch
+ * schedule).  In scenes with more than one material type, the rounds of a
+ * tile group shade through per-class lists of the round's rays, so that each
+ * wave shades one material class. Results are identical.  mode: 0 =
+ * automatic (on for such scenes in tile groups), 1 = off.
+ * ptGetBasicRendererClassLists sets *used to 1 when consecutive rounds use
+ * them now.  Default 0. */
+int                ptSetBasicRendererClassLists(pt_basic_renderer* renderer, uint32_t mode);
+int                ptGetBasicRendererClassLists(const pt_basic_renderer* renderer, uint32_t* used);
 int                ptSetBasicRendererSplit(pt_basic_renderer* renderer, uint32_t groups);
 int                ptGetBasicRendererSplit(const pt_basic_renderer* renderer, uint32_t* groups, uint32_t* timed_tiles,
                                            uint32_t* tiles);

@@ -259,6 +259,8 @@ HIP_API = {
     "ptRunBasicRendererRounds": (_i32, [_vp, _vp, _u32]),
     "ptSetBasicRendererRoundBatch": (_i32, [_vp, _u32]),
     "ptSetBasicRendererSplit": (_i32, [_vp, _u32]),
+    "ptSetBasicRendererClassLists": (_i32, [_vp, _u32]),
+    "ptGetBasicRendererClassLists": (_i32, [_vp, _u32ptr]),
     "ptGetBasicRendererSplit": (_i32, [_vp, _u32ptr, _u32ptr, _u32ptr]),
     "ptSetBasicRendererOpenPBR": (_i32, [_vp, _i32]),
     "ptGetStats": (_i32, [_vp, _vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),

@@ -1057,68 +1057,10 @@ __global__ __launch_bounds__(256) void restore_rays_kernel(dslots L, dframe F, c
 
 // Ray sources of the extend kernel: the renderer's slots, or the arrays of
 // the ray-query API.
-#if PT_EXP_CLASSQ == 2
-// Experiment build only: the last of a tile's four waves to finish extend
-// appends the tile's 256 positions to the per-class sub-lists t % CQ_SUB
-// (one atomic per class, by lanes 0..C-1 at once).  The waves hand their
-// class ballots over in LDS (lds: [0] a ticket zeroed at kernel start, then
-// 4 x C ballots); no block barrier.
-PT_DEV void ClassListAppend(const dslots& L, uint64_t* lds, uint32_t q, const uint64_t* b)
-{
-    constexpr uint32_t C = PT_OUTCOME_CLASSES;
-    uint64_t* bl = lds + 1;
-    const uint32_t w = (q >> 6) & 3u, lane = q & 63u;
-    uint64_t mine = 0;
-#pragma unroll
-    for (uint32_t c = 0; c < C; c++) if (lane == c) mine = b[c];
-    if (lane < C) bl[w * C + lane] = mine;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    uint32_t old = 0;
-    if (lane == 0) old = atomicAdd(reinterpret_cast<uint32_t*>(lds), 1u);
-    old = (uint32_t)__shfl((int)old, 0, 64);
-    if (old != 3u) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    const uint32_t tile = q >> 8, sub = tile % CQ_SUB;
-    // The ballots are wave-uniform: read into scalar registers.
-    auto U = [&](uint32_t i) -> uint64_t {
-        const uint64_t v = bl[i];
-        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-        return ((uint64_t)hi << 32) | lo;
-    };
-    uint32_t mycount = 0;
-#pragma unroll
-    for (uint32_t c = 0; c < C; c++) {
-        uint32_t t = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) t += (uint32_t)__popcll(U(k * C + c));
-        if (lane == c) mycount = t;
-    }
-    uint32_t base = 0;
-    if (lane < C && mycount) base = atomicAdd(&L.cq_counts[lane * CQ_SUB + sub], mycount);
-#pragma unroll
-    for (uint32_t c = 0; c < C; c++) {
-        const uint32_t bc = (uint32_t)__shfl((int)base, (int)c, 64);
-        uint32_t before = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) {
-            const uint64_t m = U(k * C + c);
-            if ((m >> lane) & 1ull) {
-                const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                L.cq_list[((size_t)c * CQ_SUB + sub) * L.cq_capk + bc + before + r] = tile * 256u + k * 64u + lane;
-            }
-            before += (uint32_t)__popcll(m);
-        }
-    }
-}
-#endif
 
 struct ray_source_slots {
     dslots L;
     dframe F;
-#if PT_EXP_CLASSQ == 2
-    uint64_t* cq_lds = nullptr;
-#endif
     // s is a ray POSITION (TileOrder), not a slot.
     PT_DEV bool load(uint32_t s, pt3& O, pt3& V, float& D) const
     {
@@ -1145,28 +1087,13 @@ struct ray_source_slots {
         if (!classes) {
             uint64_t b = __ballot(cls == PT_OUTCOME_CLASSES - 1);
             if ((q & 63u) == 0) m[4 * (PT_OUTCOME_CLASSES - 1)] = b;
-#if PT_EXP_CLASSQ == 2
-            if (L.cq_list) {
-                const uint64_t bs[PT_OUTCOME_CLASSES] = {~b, 0ull, 0ull, 0ull, b};
-                ClassListAppend(L, cq_lds, q, bs);
-            }
-#endif
             return;
         }
-#if PT_EXP_CLASSQ == 2
-        uint64_t bs[PT_OUTCOME_CLASSES];
-#endif
 #pragma unroll
         for (uint32_t c = 0; c < PT_OUTCOME_CLASSES; c++) {
             uint64_t b = __ballot(cls == c);
             if ((q & 63u) == 0) m[4 * c] = b;
-#if PT_EXP_CLASSQ == 2
-            bs[c] = b;
-#endif
         }
-#if PT_EXP_CLASSQ == 2
-        if (L.cq_list) ClassListAppend(L, cq_lds, q, bs);
-#endif
     }
 };
 
@@ -1305,20 +1232,6 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
             timed = true;
         }
     }
-#if PT_EXP_CLASSQ == 2
-    if constexpr (kRendererSource<Src>) {
-        __shared__ uint64_t cq_lds[1 + 4 * PT_OUTCOME_CLASSES];
-        if (src.L.cq_list) {
-            if (threadIdx.x == 0) cq_lds[0] = 0ull;
-            if (blockIdx.x == 0 && threadIdx.x < PT_OUTCOME_CLASSES * CQ_SUB) src.L.cq_next[threadIdx.x] = 0u;
-            __syncthreads();
-        }
-        Src s2 = src;
-        s2.cq_lds = cq_lds;
-        ExtendTile<Src, SPILL, CAP, E>(S, s2, n, spill, spill_stride, smem, tile, timed, ncache, ncn);
-        return;
-    }
-#endif
     ExtendTile<Src, SPILL, CAP, E>(S, src, n, spill, spill_stride, smem, tile, timed, ncache, ncn);
 }
 
@@ -1802,24 +1715,31 @@ __global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void shade_kernel(dscen
     ShadeStatsEnd();
 }
 
-#if PT_EXP_CLASSQ
-// Experiment build only: global per-class shade lists.
-// Extend appends every position of a tile to its outcome class's list
-// (ClassListAppend); shade_classq_kernel gives each block 256 entries of one
-// class, so every wave shades one class with that class's BSDF code alone.
-// New rays stay at the position they replace (no TileOrder: the slot <->
-// position map is unchanged), so results are identical.
-#if PT_EXP_CLASSQ == 1
-// PT_EXP_CLASSQ=1: the lists are built by a kernel between extend and shade.
-// A block lists CQ_TILES tiles: one wave scans the (tile, wave word) counts
-// of every class and takes the block's run of each class's list with one
-// atomic per class, lanes 0..C-1 at once (a tile per block instead: 4096
-// atomics per address per C2 round, serialised, 26 us).  Block 0 clears the
-// other parity's counters for the next round.
+// Class-pure shade (round 5).  Every position of a round
+// goes to the global list of its outcome class (extend's ShadeOrder classes:
+// hit diffuse / metal / translucent / other material, miss), and
+// shade_classq_kernel gives each block 256 entries of one class, so every
+// wave shades one class with that class's BSDF code alone (ShadeSlot's CLS).
+// A new ray stays at the position it replaces: TileOrder needs a tile's 256
+// new rays together, which a class-pure block does not hold; the slot <->
+// position map is unchanged, so the results are identical.  Used inside tile
+// groups (runtime.hip ClassLists), where the lists' latency and the gathers'
+// extra bytes overlap the other groups' launches: C2 +6 %, C5 +6 %; on one
+// stream the lists cost more than the lanes gain.
+//
+// class_list_kernel builds the lists between extend and shade.  A block
+// lists CQ_TILES tiles: one wave scans the (tile, wave word) counts of every
+// class and takes the block's run of each class's list with one atomic per
+// class, lanes 0..C-1 at once (a tile per block instead: 4096 atomics per
+// address per C2 round, serialised, 26 us).  Block 0 clears the other
+// parity's counters for the next round.
 constexpr uint32_t CQ_TILES = 16;
 __global__ __launch_bounds__(256) void class_list_kernel(dslots L, uint32_t mat_classes, uint32_t* counts,
-                                                         uint32_t* next_counts, uint32_t* list, uint32_t capk)
+                                                         uint32_t* next_counts, uint32_t* list, uint32_t capk,
+                                                         uint32_t tiles_all, uint32_t groups, uint32_t group)
 {
+    // L.tile_count tiles of tile group `group` (all tiles: groups = 1).
+    auto TILE = [&](uint32_t j) { return pt_tile_group_tile(tiles_all, groups, group, j); };
     constexpr uint32_t C = PT_OUTCOME_CLASSES;
     static_assert(CQ_SUB == 1 && 4 * CQ_TILES <= 64, "one list per class; one wave scans the block's counts");
     __shared__ uint64_t om_s[CQ_TILES * 4 * C];
@@ -1829,7 +1749,8 @@ __global__ __launch_bounds__(256) void class_list_kernel(dslots L, uint32_t mat_
     const uint32_t tile0 = blockIdx.x * CQ_TILES;
     const uint32_t ntiles = L.tile_count - tile0 < CQ_TILES ? L.tile_count - tile0 : CQ_TILES;
     if (blockIdx.x == 0 && t < C) next_counts[t] = 0u;
-    for (uint32_t i = t; i < ntiles * 4 * C; i += 256) om_s[i] = L.outcome[(size_t)tile0 * (4 * C) + i];
+    for (uint32_t i = t; i < ntiles * 4 * C; i += 256)
+        om_s[i] = L.outcome[(size_t)TILE(tile0 + i / (4 * C)) * (4 * C) + i % (4 * C)];
     __syncthreads();
     auto mask = [&](uint32_t j, uint32_t c, uint32_t k) -> uint64_t {
         const uint64_t* om = om_s + j * (4 * C);
@@ -1857,7 +1778,7 @@ __global__ __launch_bounds__(256) void class_list_kernel(dslots L, uint32_t mat_
     }
     __syncthreads();
     for (uint32_t j = 0; j < ntiles; j++) {
-        const uint32_t q = (tile0 + j) * 256 + t;
+        const uint32_t q = TILE(tile0 + j) * 256 + t;
 #pragma unroll
         for (uint32_t c = 0; c < C; c++) {
             const uint64_t m = mask(j, c, w);
@@ -1868,7 +1789,6 @@ __global__ __launch_bounds__(256) void class_list_kernel(dslots L, uint32_t mat_
         }
     }
 }
-#endif
 
 template <uint32_t MATS, bool COMPACT>
 __global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void shade_classq_kernel(dscene S, dslots L, dframe F,
@@ -1948,7 +1868,6 @@ __global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void shade_classq_kerne
         L.pos[s] = (uint16_t)(((q & 255u) << 8) | (q & 255u));
     }
 }
-#endif
 
 
 // One round (extend + shade) of a tile per block, for partitions whose tiles
@@ -2364,45 +2283,42 @@ hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd
     return hipGetLastError();
 }
 
-#if PT_EXP_CLASSQ
 template <bool COMPACT>
 static void LaunchShadeQ(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
                          uint32_t scene_mats, const uint32_t* counts, const uint32_t* list, hipStream_t st)
 {
+    // The shade instantiations of LaunchShade for scenes with more than one
+    // material type (pt_class_lists_supported); blocks past the lists return.
     const uint32_t blocks = L.tile_count + ptd::PT_OUTCOME_CLASSES;
     const uint32_t capk = pt_classq_sub_capacity(L.tile_count);
-    switch (pt_shade_mats(scene_mats)) {
-    case PT_MATS_DIFFUSE | PT_MATS_SCENE:
-        hipLaunchKernelGGL((ptd::shade_classq_kernel<PT_MATS_DIFFUSE | PT_MATS_SCENE, COMPACT>), dim3(blocks), dim3(256),
-                           0, st, S, L, F, P, counts, list, capk);
-        break;
-    case PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_SCENE:
+    if (pt_shade_mats(scene_mats) == (PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_SCENE))
         hipLaunchKernelGGL((ptd::shade_classq_kernel<PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_SCENE, COMPACT>),
                            dim3(blocks), dim3(256), 0, st, S, L, F, P, counts, list, capk);
-        break;
-    default:
+    else
         hipLaunchKernelGGL((ptd::shade_classq_kernel<PT_MATS_ALL | PT_MATS_SCENE, COMPACT>), dim3(blocks), dim3(256), 0,
                            st, S, L, F, P, counts, list, capk);
-        break;
-    }
+}
+
+bool pt_class_lists_supported(uint32_t scene_mats)
+{
+    const uint32_t m = pt_shade_mats(scene_mats);
+    return m == (PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_SCENE) || m == (PT_MATS_ALL | PT_MATS_SCENE);
 }
 
 hipError_t pt_launch_shade_classq(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F,
                                   const ptd::dparams& P, uint32_t scene_mats, bool compact, uint32_t* counts,
-                                  uint32_t* next_counts, uint32_t* list, hipStream_t st)
+                                  uint32_t* next_counts, uint32_t* list, hipStream_t st, uint32_t tiles_all,
+                                  uint32_t groups, uint32_t group)
 {
     if (L.n == 0 || L.tile_count == 0) return hipSuccess;
-#if PT_EXP_CLASSQ == 1
+    if (!pt_class_lists_supported(scene_mats)) return hipErrorNotSupported;
     hipLaunchKernelGGL(ptd::class_list_kernel, dim3((L.tile_count + ptd::CQ_TILES - 1) / ptd::CQ_TILES), dim3(256), 0,
-                       st, L, S.mat_classes, counts, next_counts, list, pt_classq_sub_capacity(L.tile_count));
-#else
-    (void)next_counts;
-#endif
+                       st, L, S.mat_classes, counts, next_counts, list, pt_classq_sub_capacity(L.tile_count),
+                       tiles_all ? tiles_all : L.tile_count, groups, group);
     if (compact) LaunchShadeQ<true>(S, L, F, P, scene_mats, counts, list, st);
     else LaunchShadeQ<false>(S, L, F, P, scene_mats, counts, list, st);
     return hipGetLastError();
 }
-#endif
 
 #if PT_SHADE_STATS
 // Experiment build only (tools/shade_stats.py): the launch-summed shade

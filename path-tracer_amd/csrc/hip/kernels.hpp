@@ -36,14 +36,6 @@ struct dslots {
     const uint32_t* stop = nullptr;   // guarded rounds (ptRenderFrame's last rounds): set -> the launch returns
     uint32_t n;
     uint32_t tile_count;    // n / 256: one block per tile
-#if PT_EXP_CLASSQ
-    // Experiment build only: extend appends each tile's positions to the
-    // per-class sub-lists (counters cq_counts, cleared: cq_next) when set.
-    uint32_t* cq_counts = nullptr;
-    uint32_t* cq_next = nullptr;
-    uint32_t* cq_list = nullptr;
-    uint32_t cq_capk = 0;
-#endif
 };
 
 struct dframe {
@@ -122,21 +114,20 @@ hipError_t pt_launch_resolve(const float4* accum, uint32_t n, float brightness, 
 // paths also end at surfaces.
 hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
                            uint32_t scene_mats, bool compact, hipStream_t st);
-#if PT_EXP_CLASSQ
-// Experiment build only: shade through global per-class lists, each class's
-// list CQ_SUB sub-lists of pt_classq_sub_capacity words; counts: the
-// PT_OUTCOME_CLASSES x CQ_SUB sub-list counters of this round (next_counts:
-// the other parity's, cleared for the next round).  PT_EXP_CLASSQ=1: a list
-// kernel runs first; 2: the round's extend built them (dslots.cq_*).
-#ifndef PT_CQ_SUB
-#define PT_CQ_SUB (PT_EXP_CLASSQ == 2 ? 8 : 1)
-#endif
-constexpr uint32_t CQ_SUB = PT_CQ_SUB;   // sub-lists per class: tile t appends to t % CQ_SUB
+// Class-pure shade (kernels.hip shade_classq_kernel): per-class lists of the
+// round's positions built by class_list_kernel, each class's list CQ_SUB
+// sub-lists of pt_classq_sub_capacity words; counts: the PT_OUTCOME_CLASSES x
+// CQ_SUB counters of this round (zero at the launch), next_counts: the other
+// parity's, cleared for the next round.  L is a tile group's slots (the
+// group's tile_count; tiles_all, groups, group: pt_tile_group_tile).  For the
+// shade instantiations pt_class_lists_supported accepts.
+constexpr uint32_t CQ_SUB = 1;
 inline uint32_t pt_classq_sub_capacity(uint32_t tiles) { return (tiles + CQ_SUB - 1) / CQ_SUB * 256; }
+bool pt_class_lists_supported(uint32_t scene_mats);
 hipError_t pt_launch_shade_classq(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F,
                                   const ptd::dparams& P, uint32_t scene_mats, bool compact, uint32_t* counts,
-                                  uint32_t* next_counts, uint32_t* list, hipStream_t st);
-#endif
+                                  uint32_t* next_counts, uint32_t* list, hipStream_t st, uint32_t tiles_all = 0,
+                                  uint32_t groups = 1, uint32_t group = 0);
 hipError_t pt_launch_vertex_decode(const uint2* v, uint32_t n, float4* attr, float* vv, hipStream_t st);
 // Tile groups (ptSetBasicRendererSplit): group g of K owns tiles g, g + K, ...
 // (pt_tile_group_count of them) and the dispatch-order segment starting at

@@ -173,10 +173,9 @@ struct pt_basic_renderer {
     bool grey = false;                  // the live paths are in the grey record form (slots.prob1 set)
     bool grey_blocked = false;          // some live path cannot take it (until the next Reset / state write)
     dbuf<uint32_t> grey_count;          // pt_launch_grey_check's result word
-#if PT_EXP_CLASSQ
-    dbuf<uint32_t> cq_counts, cq_list;  // experiment build: per-class shade lists
+    dbuf<uint32_t> cq_counts, cq_list;  // class-pure shade lists (ClassLists)
     uint32_t cq_parity = 0;
-#endif
+    uint32_t class_lists = 0;           // ptSetBasicRendererClassLists: 0 automatic, 1 off
     dbuf<float> lam;                    // lambda0 per slot (Sample is 0 between rounds)
     dbuf<float2> uv;
     dbuf<uint2> act;
@@ -1100,9 +1099,7 @@ void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
     if (!r) return;
     if (d) { (void)hipSetDevice(d->id); (void)DeviceWait(d); }
     r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->prob1.release(); r->grey_count.release();
-#if PT_EXP_CLASSQ
     r->cq_counts.release(); r->cq_list.release();
-#endif
     r->lam.release();
     r->uv.release(); r->act.release(); r->pos.release(); r->slotof.release(); r->outcome.release();
     r->tilecost.release(); r->order.release();
@@ -1210,6 +1207,22 @@ static bool RoundFused(const pt_basic_renderer* r, const ptd::dslots& g)
     return mode == 2 || g.tile_count <= cap;
 }
 
+// Class-list buffers sized for PT_MAX_SPLIT tile groups (per group: 2
+// parities x classes x CQ_SUB counters, classes x CQ_SUB sub-lists of a whole
+// frame's capacity), allocated on first use, counters zeroed.
+static int ClassListBuffers(pt_basic_renderer* r)
+{
+    if (r->cq_list.ptr) return 0;
+    const size_t nc = (size_t)ptd::PT_OUTCOME_CLASSES * CQ_SUB;
+    if (r->cq_counts.alloc(PT_MAX_SPLIT * 2 * nc) != hipSuccess ||
+        r->cq_list.alloc(PT_MAX_SPLIT * nc * pt_classq_sub_capacity(r->slots.tile_count)) != hipSuccess ||
+        hipMemset(r->cq_counts.ptr, 0, PT_MAX_SPLIT * 2 * nc * sizeof(uint32_t)) != hipSuccess) {
+        SetError("class list allocation failed");
+        return -1;
+    }
+    return 0;
+}
+
 int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
 {
     if (!d) { SetError("null device"); return -1; }
@@ -1235,27 +1248,19 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
             if (int e = EndTimed(d, ep)) return e;
         } else {
 #if PT_EXP_CLASSQ
+            // Experiment builds: class-pure shade on the single stream too
+            // (measured slower there: DESIGN.md §4).
             const size_t nc = (size_t)ptd::PT_OUTCOME_CLASSES * CQ_SUB;
-            if (!r->cq_list.ptr) {
-                if (r->cq_counts.alloc(2 * nc) != hipSuccess ||
-                    r->cq_list.alloc(nc * pt_classq_sub_capacity(L.tile_count)) != hipSuccess ||
-                    hipMemset(r->cq_counts.ptr, 0, 2 * nc * sizeof(uint32_t)) != hipSuccess) {
-                    SetError("class list allocation failed");
-                    return -1;
-                }
-            }
-            ptd::dslots LQ = L;
-            LQ.cq_counts = r->cq_counts.ptr + nc * r->cq_parity;
-            LQ.cq_next = r->cq_counts.ptr + nc * (r->cq_parity ^ 1u);
-            LQ.cq_list = r->cq_list.ptr;
-            LQ.cq_capk = pt_classq_sub_capacity(L.tile_count);
+            if (int e = ClassListBuffers(r)) return e;
+            uint32_t* cq = r->cq_counts.ptr + nc * r->cq_parity;
+            uint32_t* cq_next = r->cq_counts.ptr + nc * (r->cq_parity ^ 1u);
             r->cq_parity ^= 1u;
             if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled)) return e;
-            PT_HIP(pt_launch_extend(r->scene->d, PT_EXP_CLASSQ == 2 ? LQ : L, F, L.spill, d->stream));
+            PT_HIP(pt_launch_extend(r->scene->d, L, F, L.spill, d->stream));
             if (int e = EndTimed(d, ep)) return e;
             if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled)) return e;
-            PT_HIP(pt_launch_shade_classq(r->scene->d, L, F, P, ShadeMats(r), ShadeCompact(r), LQ.cq_counts,
-                                          LQ.cq_next, r->cq_list.ptr, d->stream));
+            PT_HIP(pt_launch_shade_classq(r->scene->d, L, F, P, ShadeMats(r), ShadeCompact(r), cq, cq_next,
+                                          r->cq_list.ptr, d->stream));
 #else
             if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled)) return e;
             PT_HIP(pt_launch_extend(r->scene->d, L, F, L.spill, d->stream));
@@ -1294,6 +1299,17 @@ static uint32_t SplitGroups(const pt_basic_renderer* r)
     if (!L.order || L.tile_count < 2 || r->split == 1) return 1;
     if (r->split >= 2) return std::min(r->split, L.tile_count);
     return (!RoundFused(r, L) && L.tile_count >= SPLIT_MIN_TILES) ? SPLIT_AUTO_GROUPS : 1u;
+}
+
+// Class-pure shade inside tile groups (kernels.hip shade_classq_kernel):
+// scenes with more than one material type whose shade instantiation has a
+// class-pure form.  In tile groups the lists' latency and the gathers' extra
+// bytes overlap the other groups' launches (C2 +6 %, C5 +6 %); alone on one
+// stream they cost more than the lanes gain, so single-stream rounds keep
+// the tile-local shade.
+static bool ClassLists(const pt_basic_renderer* r)
+{
+    return r->class_lists != 1 && r->scene->d.mat_classes != 0 && pt_class_lists_supported(ShadeMats(r));
 }
 
 // The dispatch order holds each group's tiles in its own segment; a change of
@@ -1354,6 +1370,14 @@ static int RunRoundsSplit(pt_device* d, pt_basic_renderer* r, uint64_t k, uint32
         G[g].tile_count = pt_tile_group_count(r->slots.tile_count, K, g);
         S[g] = g ? d->group_stream[g - 1] : d->stream;
     }
+    const bool lists = ClassLists(r);
+    if (lists) {
+        // Per group: 2 parities x classes counters (zero at the batch
+        // start) and a list region of classes x a whole frame's slots.
+        if (int e = ClassListBuffers(r)) return e;
+        PT_HIP(hipMemsetAsync(r->cq_counts.ptr, 0, PT_MAX_SPLIT * 2 * ptd::PT_OUTCOME_CLASSES * CQ_SUB * sizeof(uint32_t),
+                              d->stream));
+    }
     PT_HIP(hipEventRecord(d->fork_event, d->stream));
     for (uint32_t g = 1; g < K; g++) PT_HIP(hipStreamWaitEvent(S[g], d->fork_event, 0));
 #if PT_SPLIT_STAGGER
@@ -1384,7 +1408,18 @@ static int RunRoundsSplit(pt_device* d, pt_basic_renderer* r, uint64_t k, uint32
                     if (int e = EndTimed(d, ep)) return e;
                     if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled)) return e;
                 }
-                PT_HIP(pt_launch_shade(r->scene->d, G[g], F, P, mats, compact, S[g]));
+                if (lists) {
+                    // Class-pure shade: the group's own counters (parity per
+                    // round) and list region.
+                    const size_t nc = (size_t)ptd::PT_OUTCOME_CLASSES * CQ_SUB;
+                    const size_t capk = pt_classq_sub_capacity(r->slots.tile_count);
+                    uint32_t* cnt = r->cq_counts.ptr + g * 2 * nc;
+                    PT_HIP(pt_launch_shade_classq(r->scene->d, G[g], F, P, mats, compact, cnt + nc * (i & 1u),
+                                                  cnt + nc * ((i & 1u) ^ 1u), r->cq_list.ptr + g * nc * capk, S[g],
+                                                  r->slots.tile_count, K, g));
+                } else {
+                    PT_HIP(pt_launch_shade(r->scene->d, G[g], F, P, mats, compact, S[g]));
+                }
                 if (g == 0)
                     if (int e = EndTimed(d, ep)) return e;
                 if (sort) PT_HIP(pt_launch_tile_order(r->slots, S[g], K, g));
@@ -1462,6 +1497,20 @@ int ptSetBasicRendererRoundBatch(pt_basic_renderer* r, uint32_t rounds)
 {
     if (!r) { SetError("ptSetBasicRendererRoundBatch: null renderer"); return -1; }
     r->round_batch = rounds;
+    return 0;
+}
+
+int ptSetBasicRendererClassLists(pt_basic_renderer* r, uint32_t mode)
+{
+    if (!r || mode > 1) { SetError("ptSetBasicRendererClassLists: bad argument (0 automatic, 1 off)"); return -1; }
+    r->class_lists = mode;
+    return 0;
+}
+
+int ptGetBasicRendererClassLists(const pt_basic_renderer* r, uint32_t* used)
+{
+    if (!r || !used) { SetError("ptGetBasicRendererClassLists: null argument"); return -1; }
+    *used = (SplitGroups(r) > 1 && ClassLists(r)) ? 1u : 0u;
     return 0;
 }
 

@@ -295,6 +295,17 @@ class BasicRenderer:
                "ptGetBasicRendererSplit")
         return {"groups": int(g.value), "timed_tiles": int(t0.value), "tiles": int(t.value)}
 
+    def set_class_lists(self, mode: int):
+        """Class-pure shade inside tile groups (ptSetBasicRendererClassLists):
+        0 automatic, 1 off.  Results are identical either way."""
+        _check(N.hip_lib().ptSetBasicRendererClassLists(self._h, int(mode)), "ptSetBasicRendererClassLists")
+
+    def class_lists(self) -> bool:
+        """Whether consecutive rounds shade through per-class lists now."""
+        u = C.c_uint32(0)
+        _check(N.hip_lib().ptGetBasicRendererClassLists(self._h, C.byref(u)), "ptGetBasicRendererClassLists")
+        return bool(u.value)
+
     def run_rounds(self, count: int):
         """count consecutive Run(1) calls (one new FrameIndex each), batched
         per set_round_batch (ptRunBasicRendererRounds)."""

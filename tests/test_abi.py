@@ -85,5 +85,7 @@ def test_null_arguments_rejected(pt):
     assert L.ptReadBasicRendererStreamAccumulator(None, None, 0, None) != 0
     assert L.ptSetBasicRendererSplit(None, 2) != 0
     assert L.ptGetBasicRendererSplit(None, None, None, None) != 0
+    assert L.ptSetBasicRendererClassLists(None, 0) != 0
+    assert L.ptGetBasicRendererClassLists(None, None) != 0
     out = np.zeros(1, dtype=pt._native.HIT_RECORD_DTYPE)
     assert L.ptTraceRays(None, None, 1, None, None, None, out.ctypes.data) != 0

@@ -233,3 +233,58 @@ def test_split_after_resume(pt, dev):
     b.close()
     sb.close()
     ds.close()
+
+
+@pytest.mark.parametrize("config,W,H", [(2, 96, 96), (5, 128, 64)])
+def test_class_lists_in_groups(pt, dev, config, W, H):
+    """Class-pure shade (per-class lists) inside tile groups, on scenes with
+    several material types: on and off give the same bits, both equal to the
+    unsplit rounds; the query reports when the lists are used."""
+    s = scene_for(pt, config)
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    ref = render(pt, dev, ds, W, H, [1, 1], [6, 5])
+    out = {}
+    for mode in (0, 1):
+        sb = pt.SampleBuffer(dev, W, H)
+        r = pt.BasicRenderer(dev, ds, sb)
+        r.RenderFlags = 3
+        r.set_fused_rounds(0)
+        r.set_class_lists(mode)
+        r.set_split(3)
+        assert r.class_lists() == (mode == 0)
+        r.set_split(1)
+        assert not r.class_lists()
+        r.set_split(3)
+        r.reset()
+        r.run(2)
+        r.run_rounds(6)
+        r.run_rounds(5)
+        dev.synchronize()
+        out[mode] = (r.read_state(), sb.read(), r.stats())
+        r.close()
+        sb.close()
+    for mode in (0, 1):
+        same(out[mode], ref)
+    with pytest.raises(pt.PathTracerError):
+        sb = pt.SampleBuffer(dev, W, H)
+        r = pt.BasicRenderer(dev, ds, sb)
+        try:
+            r.set_class_lists(2)
+        finally:
+            r.close()
+            sb.close()
+    ds.close()
+
+
+def test_class_lists_not_for_single_material(pt, dev):
+    """The C3 room (one material type) never takes the lists."""
+    s = scene_for(pt, 3)
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    sb = pt.SampleBuffer(dev, 1920, 1080)
+    r = pt.BasicRenderer(dev, ds, sb)
+    assert r.split()["groups"] == 3 and not r.class_lists()
+    r.close()
+    sb.close()
+    ds.close()
