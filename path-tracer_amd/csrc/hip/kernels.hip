@@ -1739,6 +1739,7 @@ __global__ __launch_bounds__(256) void class_list_kernel(dslots L, uint32_t mat_
                                                          uint32_t tiles_all, uint32_t groups, uint32_t group)
 {
     // L.tile_count tiles of tile group `group` (all tiles: groups = 1).
+    if (L.stop && *L.stop) return;   // a guarded round past the frame's target
     auto TILE = [&](uint32_t j) { return pt_tile_group_tile(tiles_all, groups, group, j); };
     constexpr uint32_t C = PT_OUTCOME_CLASSES;
     static_assert(CQ_SUB == 1 && 4 * CQ_TILES <= 64, "one list per class; one wave scans the block's counts");
@@ -1798,6 +1799,7 @@ __global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void shade_classq_kerne
                                                                                          uint32_t capk)
 {
     constexpr uint32_t C = PT_OUTCOME_CLASSES;
+    if (L.stop && *L.stop) return;   // a guarded round past the frame's target
     // Sub-list starts and class totals from the CQ_SUB x C counters
     // (uniform scalar loads; no barrier).
     uint32_t pre[C][CQ_SUB], tot[C];

@@ -36,6 +36,10 @@ struct dslots {
     const uint32_t* stop = nullptr;   // guarded rounds (ptRenderFrame's last rounds): set -> the launch returns
     uint32_t n;
     uint32_t tile_count;    // n / 256: one block per tile
+#if PT_DSLOTS_PAD
+    uint32_t* pad_[3] = {};  // A/B builds: the kernel-argument layout of the class-list experiment build
+    uint32_t pad_n_ = 0;
+#endif
 };
 
 struct dframe {

@@ -1209,17 +1209,42 @@ static bool RoundFused(const pt_basic_renderer* r, const ptd::dslots& g)
 
 // Class-list buffers sized for PT_MAX_SPLIT tile groups (per group: 2
 // parities x classes x CQ_SUB counters, classes x CQ_SUB sub-lists of a whole
-// frame's capacity), allocated on first use, counters zeroed.
+// frame's capacity) plus the counters of single-stream rounds (region
+// PT_MAX_SPLIT, kept zero by its own parity), allocated on first use, zeroed.
 static int ClassListBuffers(pt_basic_renderer* r)
 {
     if (r->cq_list.ptr) return 0;
     const size_t nc = (size_t)ptd::PT_OUTCOME_CLASSES * CQ_SUB;
-    if (r->cq_counts.alloc(PT_MAX_SPLIT * 2 * nc) != hipSuccess ||
+    if (r->cq_counts.alloc((PT_MAX_SPLIT + 1) * 2 * nc) != hipSuccess ||
         r->cq_list.alloc(PT_MAX_SPLIT * nc * pt_classq_sub_capacity(r->slots.tile_count)) != hipSuccess ||
-        hipMemset(r->cq_counts.ptr, 0, PT_MAX_SPLIT * 2 * nc * sizeof(uint32_t)) != hipSuccess) {
+        hipMemset(r->cq_counts.ptr, 0, (PT_MAX_SPLIT + 1) * 2 * nc * sizeof(uint32_t)) != hipSuccess) {
         SetError("class list allocation failed");
         return -1;
     }
+    return 0;
+}
+
+static bool ClassListRounds(const pt_basic_renderer* r);
+
+// Class-pure shade of one single-stream round over every tile (the
+// renderer's rounds outside tile groups: Run(2), single rounds, guarded
+// rounds), with the single-stream counter region.  A renderer whose tile
+// groups use the lists takes them for every round: a tile-local shade's
+// TileOrder would leave the slots permuted within their tiles against the
+// positions, and the class lists' gathers by slot lose their coherence
+// (C2 -4 % measured, profiles/r05_exp2).
+static int ClassListShade(pt_device* d, pt_basic_renderer* r, const ptd::dslots& L, const ptd::dframe& F,
+                          const ptd::dparams& P, hipStream_t st)
+{
+    if (int e = ClassListBuffers(r)) return e;
+    const size_t nc = (size_t)ptd::PT_OUTCOME_CLASSES * CQ_SUB;
+    uint32_t* cnt = r->cq_counts.ptr + PT_MAX_SPLIT * 2 * nc;
+    uint32_t* cq = cnt + nc * r->cq_parity;
+    uint32_t* cq_next = cnt + nc * (r->cq_parity ^ 1u);
+    r->cq_parity ^= 1u;
+    (void)d;
+    PT_HIP(pt_launch_shade_classq(r->scene->d, L, F, P, ShadeMats(r), ShadeCompact(r), cq, cq_next, r->cq_list.ptr,
+                                  st));
     return 0;
 }
 
@@ -1247,27 +1272,15 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
             PT_HIP(pt_launch_round(r->scene->d, L, F, P, ShadeMats(r), d->stream));
             if (int e = EndTimed(d, ep)) return e;
         } else {
-#if PT_EXP_CLASSQ
-            // Experiment builds: class-pure shade on the single stream too
-            // (measured slower there: DESIGN.md §4).
-            const size_t nc = (size_t)ptd::PT_OUTCOME_CLASSES * CQ_SUB;
-            if (int e = ClassListBuffers(r)) return e;
-            uint32_t* cq = r->cq_counts.ptr + nc * r->cq_parity;
-            uint32_t* cq_next = r->cq_counts.ptr + nc * (r->cq_parity ^ 1u);
-            r->cq_parity ^= 1u;
             if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled)) return e;
             PT_HIP(pt_launch_extend(r->scene->d, L, F, L.spill, d->stream));
             if (int e = EndTimed(d, ep)) return e;
             if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled)) return e;
-            PT_HIP(pt_launch_shade_classq(r->scene->d, L, F, P, ShadeMats(r), ShadeCompact(r), cq, cq_next,
-                                          r->cq_list.ptr, d->stream));
-#else
-            if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled)) return e;
-            PT_HIP(pt_launch_extend(r->scene->d, L, F, L.spill, d->stream));
-            if (int e = EndTimed(d, ep)) return e;
-            if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled)) return e;
-            PT_HIP(pt_launch_shade(r->scene->d, L, F, P, ShadeMats(r), ShadeCompact(r), d->stream));
-#endif
+            if (ClassListRounds(r)) {
+                if (int e = ClassListShade(d, r, L, F, P, d->stream)) return e;
+            } else {
+                PT_HIP(pt_launch_shade(r->scene->d, L, F, P, ShadeMats(r), ShadeCompact(r), d->stream));
+            }
             if (int e = EndTimed(d, ep)) return e;
         }
         if (sort)
@@ -1311,6 +1324,10 @@ static bool ClassLists(const pt_basic_renderer* r)
 {
     return r->class_lists != 1 && r->scene->d.mat_classes != 0 && pt_class_lists_supported(ShadeMats(r));
 }
+
+// Rounds of this renderer shade through class lists (tile groups and
+// single-stream rounds alike).
+static bool ClassListRounds(const pt_basic_renderer* r) { return SplitGroups(r) > 1 && ClassLists(r); }
 
 // The dispatch order holds each group's tiles in its own segment; a change of
 // K restarts it from the natural order of each group.
@@ -1510,7 +1527,7 @@ int ptSetBasicRendererClassLists(pt_basic_renderer* r, uint32_t mode)
 int ptGetBasicRendererClassLists(const pt_basic_renderer* r, uint32_t* used)
 {
     if (!r || !used) { SetError("ptGetBasicRendererClassLists: null argument"); return -1; }
-    *used = (SplitGroups(r) > 1 && ClassLists(r)) ? 1u : 0u;
+    *used = ClassListRounds(r) ? 1u : 0u;
     return 0;
 }
 
@@ -1586,6 +1603,8 @@ static int RunGuardedRounds(pt_device* d, pt_basic_renderer* r, uint32_t n, uint
     const uint32_t mats = ShadeMats(r);
     const bool compact = ShadeCompact(r);
     const uint64_t base = r->params.FrameIndex;
+    const bool lists = !fused && ClassListRounds(r);
+    const uint32_t parity0 = r->cq_parity;
     for (uint32_t i = 0; i < n; i++) {
         PT_HIP(pt_launch_guard(r->done.ptr, r->slots.n / 64 + 1, target, r->guard.ptr, d->stream));
         const ptd::dparams P = Params(r, base + i + 1);
@@ -1593,13 +1612,20 @@ static int RunGuardedRounds(pt_device* d, pt_basic_renderer* r, uint32_t n, uint
             PT_HIP(pt_launch_round(r->scene->d, L, F, P, mats, d->stream));
         } else {
             PT_HIP(pt_launch_extend(r->scene->d, L, F, L.spill, d->stream));
-            PT_HIP(pt_launch_shade(r->scene->d, L, F, P, mats, compact, d->stream));
+            if (lists) {
+                if (int e = ClassListShade(d, r, L, F, P, d->stream)) return e;
+            } else {
+                PT_HIP(pt_launch_shade(r->scene->d, L, F, P, mats, compact, d->stream));
+            }
         }
     }
     uint32_t flags[2] = {0, 0};
     PT_WAIT(d);
     PT_HIP(hipMemcpy(flags, r->guard.ptr, sizeof(flags), hipMemcpyDeviceToHost));
     *ran = flags[1];
+    // A skipped round left the class-list counters alone: the parity
+    // follows the rounds that ran.
+    if (lists) r->cq_parity = parity0 ^ (flags[1] & 1u);
     r->params.FrameIndex = base + flags[1];
     r->rays += r->valid_slots * flags[1];
     d->run_tick += flags[1];

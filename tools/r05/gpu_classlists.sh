@@ -1,8 +1,8 @@
-# Class-pure shade in tile groups as the product path: the whole GPU suite,
+# Class-pure shade for list-using renderers (tile groups and their single-stream rounds): the whole GPU suite,
 # then bench A/B of --class-lists 0 (automatic: on for C2 / C5) against 1
 # (off), interleaved, C2 and C5; C3 once (single material: unaffected).
 set -e
-O=gpurun_out/r05_classlists; mkdir -p $O
+O=gpurun_out/${TAG:-r05_classlists}; mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
 tail -2 $O/gpu_tests.log
 for c in 2 5; do
