@@ -28,7 +28,7 @@ def load(path):
 
 
 def short(name):
-    for k in ("extend", "shade", "raygen", "finalize", "rounds", "round"):
+    for k in ("class_list", "shade_classq", "extend", "shade", "raygen", "finalize", "rounds", "round"):
         if f"{k}_kernel" in name:
             return k
     return name[:40]
@@ -40,6 +40,12 @@ def main():
     for p in paths:
         for k, d in load(p).items():
             kernels.setdefault(short(k), {}).update(d)
+    # Class-pure shade (a class_list launch, then a shade_classq launch, per
+    # round and tile group): "shade" is the pair -- counters summed -- so
+    # bench.py's shade time (both launches) meets its bytes.
+    if "class_list" in kernels and "shade_classq" in kernels and "shade" not in kernels:
+        a, b = kernels["class_list"], kernels["shade_classq"]
+        kernels["shade"] = {c: a.get(c, 0.0) + b[c] for c in b}
     result = {}
     for k, d in kernels.items():
         e = {c: round(v, 1) for c, v in d.items()}
