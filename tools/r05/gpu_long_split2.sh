@@ -2,7 +2,7 @@
 # scenes (320x240, 400 rounds, three forced groups), C2's whole 256-spp
 # frame's rounds (653) and 400 rounds of C5, all in 50-round batches.
 set -u
-O=gpurun_out/r05_long_split2
+O=gpurun_out/${TAG:-r05_long_split2}
 mkdir -p "$O"
 for s in $(seq 0 23); do
   timeout -k 10 200 python3 -u tools/long_parity.py fuzz:$s 400 --batched --split 3 > "$O/fuzz_$s.json" 2> "$O/fuzz_$s.err" \
