@@ -94,7 +94,8 @@ def main():
         bad[f] = int(np.sum(np.any((g[f].view(np.uint32) != want[f].view(np.uint32)).reshape(H, W, -1), axis=-1)))
     acc_bad = int(np.sum(np.any(sb.read().view(np.uint32) != o.accum().view(np.uint32), axis=-1)))
     print(json.dumps({"config": cfg, "camera": camera, "size": [W, H], "rounds": rounds, "batched": batched,
-                      "split": r.split() if batched else None, "state_mismatch_px": bad,
+                      "split": r.split() if batched else None,
+                      "class_lists": r.class_lists() if batched else None, "state_mismatch_px": bad,
                       "accum_mismatch_px": acc_bad, "samples": float(o.accum()[..., 3].sum()),
                       "seconds": round(time.time() - t0, 1)}), flush=True)
 
