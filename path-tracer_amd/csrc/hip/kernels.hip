@@ -1055,6 +1055,25 @@ __global__ __launch_bounds__(256) void restore_rays_kernel(dslots L, dframe F, c
     TileOrderStoreKeyed(L, s, key, r, 0u);
 }
 
+// TileOrder after a class-pure shade (which leaves each new ray at the
+// position it replaced): the tile's new rays sorted by direction octant as
+// TileOrderStoreRay sorts them in the tile-local shade, for the next extend's
+// coherence.  Every ray and slot of the tile is read before any moves; the
+// hit byte is the position each slot's consumed ray (and its hit) sat at.
+__global__ __launch_bounds__(256) void tile_reorder_kernel(dslots L, dframe F, uint32_t tiles_all, uint32_t groups,
+                                                           uint32_t group)
+{
+    if (L.stop && *L.stop) return;   // a guarded round past the frame's target
+    const uint32_t tile = pt_tile_group_tile(tiles_all, groups, group, blockIdx.x);
+    const uint32_t p = tile * 256 + threadIdx.x;
+    const uint32_t s = tile * 256 + L.slotof[p];
+    const float4 r = L.ray[p];
+    uint32_t x, y;
+    const uint32_t key = TileOrderKey(SlotPixel(F, s, x, y), UnpackUnitVector(__float_as_uint(r.w)));
+    __syncthreads();
+    TileOrderStoreKeyed(L, s, key, r, threadIdx.x);
+}
+
 // Ray sources of the extend kernel: the renderer's slots, or the arrays of
 // the ray-query API.
 
@@ -2299,6 +2318,15 @@ static void LaunchShadeQ(const ptd::dscene& S, const ptd::dslots& L, const ptd::
     else
         hipLaunchKernelGGL((ptd::shade_classq_kernel<PT_MATS_ALL | PT_MATS_SCENE, COMPACT>), dim3(blocks), dim3(256), 0,
                            st, S, L, F, P, counts, list, capk);
+}
+
+hipError_t pt_launch_tile_reorder(const ptd::dslots& L, const ptd::dframe& F, uint32_t tiles_all, uint32_t groups,
+                                  uint32_t group, hipStream_t st)
+{
+    if (L.n == 0 || L.tile_count == 0) return hipSuccess;
+    hipLaunchKernelGGL(ptd::tile_reorder_kernel, dim3(L.tile_count), dim3(256), 0, st, L, F,
+                       tiles_all ? tiles_all : L.tile_count, groups, group);
+    return hipGetLastError();
 }
 
 bool pt_class_lists_supported(uint32_t scene_mats)

@@ -128,6 +128,12 @@ hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd
 constexpr uint32_t CQ_SUB = 1;
 inline uint32_t pt_classq_sub_capacity(uint32_t tiles) { return (tiles + CQ_SUB - 1) / CQ_SUB * 256; }
 bool pt_class_lists_supported(uint32_t scene_mats);
+// TileOrder of a tile group's new rays after a class-pure shade.
+hipError_t pt_launch_tile_reorder(const ptd::dslots& L, const ptd::dframe& F, uint32_t tiles_all, uint32_t groups,
+                                  uint32_t group, hipStream_t st);
+#ifndef PT_LIST_REORDER
+#define PT_LIST_REORDER 0   // A/B builds: 1 = re-sort the rays by octant after each class-pure shade
+#endif
 hipError_t pt_launch_shade_classq(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F,
                                   const ptd::dparams& P, uint32_t scene_mats, bool compact, uint32_t* counts,
                                   uint32_t* next_counts, uint32_t* list, hipStream_t st, uint32_t tiles_all = 0,

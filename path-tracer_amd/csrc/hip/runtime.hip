@@ -1245,6 +1245,7 @@ static int ClassListShade(pt_device* d, pt_basic_renderer* r, const ptd::dslots&
     (void)d;
     PT_HIP(pt_launch_shade_classq(r->scene->d, L, F, P, ShadeMats(r), ShadeCompact(r), cq, cq_next, r->cq_list.ptr,
                                   st));
+    if (PT_LIST_REORDER) PT_HIP(pt_launch_tile_reorder(L, F, 0, 1, 0, st));
     return 0;
 }
 
@@ -1434,6 +1435,7 @@ static int RunRoundsSplit(pt_device* d, pt_basic_renderer* r, uint64_t k, uint32
                     PT_HIP(pt_launch_shade_classq(r->scene->d, G[g], F, P, mats, compact, cnt + nc * (i & 1u),
                                                   cnt + nc * ((i & 1u) ^ 1u), r->cq_list.ptr + g * nc * capk, S[g],
                                                   r->slots.tile_count, K, g));
+                    if (PT_LIST_REORDER) PT_HIP(pt_launch_tile_reorder(G[g], F, r->slots.tile_count, K, g, S[g]));
                 } else {
                     PT_HIP(pt_launch_shade(r->scene->d, G[g], F, P, mats, compact, S[g]));
                 }
