@@ -142,45 +142,60 @@ def pick_cores(n, sample_s=0.25):
                          f"over a {sample_s} s /proc/stat sample (mean busy {best[0] / n:.2f})")
 
 
-def cpu_baseline(pt, scene, width, height, config, settle_rounds=34, min_rounds=32, max_seconds=30.0):
-    """Time the CPU oracle (scalar C++ restatement, std::thread over host
-    cores) on the same scene and frame.  Bounded: Reset + Run(2) and
-    `settle_rounds` untimed rounds (the path population past its first,
-    shortest rounds: the per-round cost is then stationary, as in
-    tools/cpu_scaling.py), then at least `min_rounds` timed single rounds,
-    more while under max_seconds.
+CPU_SETTLE_ROUNDS = 34   # the CPU leg's settled window starts after Reset + Run(2) + this many rounds
 
-    Threads: every CPU this process may run on (its affinity mask), capped by
-    OMP_NUM_THREADS when set -- on the GPU box that is the job's CPU share
-    (16) of a machine whose nproc counts every GPU's share."""
-    sys.path.insert(0, str(ROOT / "tests"))
-    import oracle_lib
+
+def cpu_threads():
+    """The CPU leg's thread count: every CPU this process may run on (its
+    affinity mask), capped by OMP_NUM_THREADS when set -- on the GPU box that
+    is the job's CPU share (16) of a machine whose nproc counts every GPU's
+    share.  Returns (threads, affinity CPUs, OMP_NUM_THREADS or 0)."""
     host_cpus = os.cpu_count() or 1
     try:
         allowed = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         allowed = host_cpus
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    threads = max(1, min(allowed, omp) if omp > 0 else allowed)
-    # The oracle's worker threads are created per round and inherit this
-    # thread's mask: pin it to `threads` distinct cores for the measurement.
-    home = os.sched_getaffinity(0)
-    pinned, placement = pick_cores(threads) if threads < allowed else (None, "every affinity CPU, unpinned")
+    return max(1, min(allowed, omp) if omp > 0 else allowed), allowed, omp
+
+
+def settled_oracle(scene, width, height, threads, flags, settle_rounds=CPU_SETTLE_ROUNDS):
+    """The CPU oracle on the frame, past its first rounds: Reset, Run(2) and
+    `settle_rounds` untimed rounds (the path population past its first,
+    shortest paths; the per-round cost is then stationary)."""
+    sys.path.insert(0, str(ROOT / "tests"))
+    import oracle_lib  # test infrastructure: the CPU baseline, never the product path
     o = oracle_lib.OracleRenderer(scene.packs(), width, height, threads=threads)
+    o.RenderFlags = flags
+    o.reset()
+    o.run(2)
+    for _ in range(settle_rounds):
+        o.run(1)
+    return o
+
+
+def time_oracle_rounds(o, threads, min_rounds=32, max_seconds=30.0):
+    """Time consecutive single rounds of a settled oracle at `threads`
+    threads, pinned to that many distinct physical cores of one package
+    (pick_cores) unless that is every affinity CPU: at least min_rounds, more
+    while under max_seconds / 2, never past max_seconds.  The one timing
+    code path of bench.py's CPU leg and tools/cpu_scaling.py's table."""
+    home = os.sched_getaffinity(0)
+    o.set_threads(threads)
+    # The oracle's worker threads are created per round and inherit this
+    # thread's mask.
+    pinned, placement = pick_cores(threads) if threads < len(home) else (None, "every affinity CPU, unpinned")
     try:
         if pinned:
             os.sched_setaffinity(0, pinned)
-        o.RenderFlags = 3
-        o.reset()
-        o.run(2)
-        for _ in range(settle_rounds):
-            o.run(1)
         r0, s0 = o.counters()
         t0 = time.perf_counter()
         c0 = time.process_time()
-        rounds = 0
+        rounds, per_round = 0, []
         while rounds < min_rounds or time.perf_counter() - t0 < max_seconds / 2:
+            t1 = time.perf_counter()
             o.run(1)
+            per_round.append(time.perf_counter() - t1)
             rounds += 1
             if time.perf_counter() - t0 > max_seconds:
                 break
@@ -189,10 +204,33 @@ def cpu_baseline(pt, scene, width, height, config, settle_rounds=34, min_rounds=
         r1, s1 = o.counters()
     finally:
         os.sched_setaffinity(0, home)
+    per_round.sort()
+    return {"threads": threads, "rounds": rounds, "seconds": round(dt, 3), "rays": r1 - r0, "samples": s1 - s0,
+            "mrays_per_s": round((r1 - r0) / dt / 1e6, 4), "msamples_per_s": round((s1 - s0) / dt / 1e6, 4),
+            "median_round_s": round(per_round[len(per_round) // 2], 4),
+            "min_round_s": round(per_round[0], 4), "max_round_s": round(per_round[-1], 4),
+            # CPU seconds the process's threads actually ran (= threads x
+            # wall time when the pinned cores were not shared).
+            "cpu_seconds": round(cpu_s, 2),
+            "mrays_per_cpu_s_x_threads": round((r1 - r0) / max(cpu_s, 1e-9) * threads / 1e6, 4),
+            "placement": placement, "pinned_cpus": sorted(pinned) if pinned else None}
+
+
+def cpu_baseline(pt, scene, width, height, config, settle_rounds=CPU_SETTLE_ROUNDS, min_rounds=32, max_seconds=30.0):
+    """Time the CPU oracle (scalar C++ restatement, std::thread over host
+    cores) on the same scene and frame: settled_oracle, then
+    time_oracle_rounds at the job's thread count (cpu_threads).  Bounded:
+    about 15-30 s of CPU work."""
+    threads, allowed, omp = cpu_threads()
+    host_cpus = os.cpu_count() or 1
+    o = settled_oracle(scene, width, height, threads, 3, settle_rounds)
+    try:
+        row = time_oracle_rounds(o, threads, min_rounds, max_seconds)
+    finally:
         o.close()
     share = "the job's CPU share (OMP_NUM_THREADS)" if omp > 0 and omp < allowed else "every affinity CPU"
     return {
-        "value": round((r1 - r0) / dt / 1e6, 4),
+        "value": row["mrays_per_s"],
         "unit": "Mrays/s",
         "cores": threads,
         "threads": threads,
@@ -200,17 +238,17 @@ def cpu_baseline(pt, scene, width, height, config, settle_rounds=34, min_rounds=
         "host_cpus": host_cpus,
         "affinity_cpus": allowed,
         "omp_num_threads": omp or None,
-        "placement": placement,
-        "pinned_cpus": sorted(pinned) if pinned else None,
+        "placement": row["placement"],
+        "pinned_cpus": row["pinned_cpus"],
         "cpu_model": cpu_model(),
         "kind": "port",
-        "sample": f"C{config} {width}x{height}, {rounds} consecutive rounds after Reset + Run(2) + "
-                  f"{settle_rounds} settle rounds ({(r1 - r0)} rays, {(s1 - s0)} samples, {dt:.1f} s timed)",
-        "msamples_per_s": round((s1 - s0) / dt / 1e6, 4),
-        # CPU seconds the process's threads actually ran (= threads x wall
-        # time when the pinned cores were not shared).
-        "cpu_seconds": round(cpu_s, 2),
-        "mrays_per_cpu_s_x_threads": round((r1 - r0) / max(cpu_s, 1e-9) * threads / 1e6, 4),
+        "sample": f"C{config} {width}x{height}, {row['rounds']} consecutive rounds after Reset + Run(2) + "
+                  f"{settle_rounds} settle rounds ({row['rays']} rays, {row['samples']} samples, "
+                  f"{row['seconds']:.1f} s timed)",
+        "msamples_per_s": row["msamples_per_s"],
+        "median_round_s": row["median_round_s"],
+        "cpu_seconds": row["cpu_seconds"],
+        "mrays_per_cpu_s_x_threads": row["mrays_per_cpu_s_x_threads"],
     }
 
 
@@ -515,20 +553,23 @@ def main():
     prof = profile_for(pkey) or {}
     kprof = prof.get("kernels", {}).get(dom, {})
     traffic = kprof.get("hbm_bytes")
-    # The roofline that binds the dominant kernel: its
-    # committed PMC's VALU issue fraction x active lanes / 64 (the fraction of
-    # the chip's lane-issue capacity doing useful work) against the HBM
-    # fraction its measured traffic reaches; the larger names the binding
-    # resource.  `frac` stays the algorithmic-bytes HBM fraction, comparable
-    # across rounds.
+    # The roofline that binds the dominant kernel,
+    # from the committed PMC of this workload, every figure in ONE machine
+    # state -- the profiled dispatches, which rocprofv3 serialises:
+    #   issue_frac   = VALU issue fraction x active lanes / 64 (the chip's
+    #                  lane-issue capacity doing useful work),
+    #   traffic_frac = the dispatches' HBM bytes / their own duration / peak.
+    # Whichever resource is closer to its peak in that state binds; `bound`
+    # says which, and the line's frac stays priced against HBM.
     dissue = (prof.get("issue") or {}).get(dom) or {}
     issue_frac = (round(dissue["valu_issue_frac"] * dissue["valu_active_lanes"] / 64.0, 4)
                   if "valu_issue_frac" in dissue and "valu_active_lanes" in dissue else None)
-    traffic_frac = (round(traffic / (kernels[dom]["avg_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
-                    if traffic is not None else None)
-    if issue_frac is None or traffic_frac is None:
+    dispatch_ms = kprof.get("dispatch_ms")
+    traffic_frac = (round(traffic / (dispatch_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+                    if traffic is not None and dispatch_ms else None)
+    if "valu_issue_frac" not in dissue or traffic_frac is None:
         binding = None
-    elif dissue.get("valu_issue_frac", 0) > traffic_frac:
+    elif dissue["valu_issue_frac"] > traffic_frac:
         binding = "valu_issue"
     else:
         binding = "hbm"
@@ -537,7 +578,8 @@ def main():
     # sample shards and band path streams add independent RNG streams
     # (FrameIndex offsets), the same estimator with the same sample count.
     if world == 1 and streams == 1:
-        identity = "bit-identical to the reference integrator's frame (oracle-checked at every config)"
+        identity = ("bit-identical to the oracle's frame (the CPU restatement of the reference integrator; "
+                    "tests/test_gpu_bench_path.py checks this schedule at full size)")
     elif shard == "bands" and streams == 1:
         identity = "bit-identical to the 1-GPU frame (disjoint bands, same seeds)"
     else:
@@ -598,28 +640,34 @@ def main():
         },
         "steady_state": steady,
         "roofline": {
-            "bound": "hbm",
+            # The limiter of the dominant kernel in its profiled state (HBM
+            # or VALU issue); peak / frac are the HBM roofline either way.
+            "bound": binding or "hbm",
+            "priced_against": "hbm",
             "kernel": dom,
-            "achieved": round(achieved, 2),
+            # The dominant kernel's share of the chip: the frame's wall time
+            # per round apportioned among the kernels by their summed launch
+            # time per round (tile groups run K launches of each kernel
+            # concurrently), its algorithmic bytes per round over that share.
+            # Kernel time <= step time by construction.
+            "achieved": apportioned["achieved"] if apportioned else round(achieved, 2),
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 5),
+            "frac": apportioned["frac"] if apportioned else round(achieved / HBM_PEAK_GBPS, 5),
+            "frac_basis": "apportioned chip share per round" if apportioned else "per launch",
             "traffic": traffic,
             "traffic_unit": "bytes per launch (HBM, PMC)",
             "traffic_source": prof.get("profile") if traffic is not None else None,
             "alg_bytes_per_launch": round(ALG_BYTES[dom] * launch_slots),
-            # Tile groups: that many launches of each kernel run concurrently
-            # per round (one per group's stream); a launch covers
-            # slots_per_timed_launch slots, and its rate is its own bytes over
-            # its own duration (path_frac is the whole frame's).
+            "alg_bytes_per_round": round(ALG_BYTES[dom] * slots_owned),
             "split_groups": split["groups"],
             "slots_per_timed_launch": round(launch_slots),
-            # The frame's wall time per round shared among the kernels in
-            # proportion to their summed launch time per round (groups x a
-            # group's launch): with tile groups the launches overlap, so this
-            # is the dominant kernel's share of the chip, comparable with an
-            # unsplit launch's time.
             "apportioned": apportioned,
+            # One timed launch's own rate: its bytes over its own duration.
+            # With tile groups, `split_groups` such launches overlap, so this
+            # is not a share of the chip (secondary).
+            "per_launch": {"avg_ms": round(kernels[dom]["avg_ms"], 4), "achieved": round(achieved, 2),
+                           "frac": round(achieved / HBM_PEAK_GBPS, 5)},
             "alg_bytes_per_slot": ALG_BYTES[dom],
             "launch_avg_ms": {k: round(v["avg_ms"], 4) for k, v in kernels.items()},
             "launches_timed": {**{k: v[0] for k, v in kstats.items()}, "every_nth_round": args.profile_period},
@@ -627,10 +675,11 @@ def main():
             "path_gbps_220B_per_ray": round(PATH_BYTES_PER_RAY * rays / dt / 1e9, 2),
             # BASELINE.md's whole-path definition: 220 B per ray over the frame time.
             "path_frac": round(PATH_BYTES_PER_RAY * rays / dt / 1e9 / HBM_PEAK_GBPS, 5),
-            # The dominant kernel's measured HBM traffic (PMC) over its launch time.
+            # Both from the committed PMC's serialised dispatches (above).
             "traffic_frac": traffic_frac,
-            # valu_issue_frac x active lanes / 64 from the same committed PMC.
             "issue_frac": issue_frac,
+            "pmc_state": "serialised profiled dispatches (rocprofv3 --pmc): counters and durations of the same dispatches",
+            "pmc_dispatch_ms": dispatch_ms,
             "binding": binding,
         },
         # What bounds the dominant kernel instead of HBM (PMC of this config's

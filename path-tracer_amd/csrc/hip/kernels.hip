@@ -1016,10 +1016,6 @@ PT_DEV bool Scatter(const dscene& S, rng& G, float PTP, path& Path, pt3& O, pt3&
 
 // --- kernels -------------------------------------------------------------------
 
-#ifndef PT_WAVE_PRIO
-#define PT_WAVE_PRIO 0
-#endif
-
 // One block per tile (the slot count is a multiple of 256): TileOrder needs
 // every thread of the block, so no thread returns early.
 
@@ -1053,25 +1049,6 @@ __global__ __launch_bounds__(256) void restore_rays_kernel(dslots L, dframe F, c
     L.hit[s] = make_float4(0.0f, __uint_as_float(SHAPE_INDEX_NONE), 0.0f, 0.0f);
     L.uv[s] = make_float2(0.0f, 0.0f);
     TileOrderStoreKeyed(L, s, key, r, 0u);
-}
-
-// TileOrder after a class-pure shade (which leaves each new ray at the
-// position it replaced): the tile's new rays sorted by direction octant as
-// TileOrderStoreRay sorts them in the tile-local shade, for the next extend's
-// coherence.  Every ray and slot of the tile is read before any moves; the
-// hit byte is the position each slot's consumed ray (and its hit) sat at.
-__global__ __launch_bounds__(256) void tile_reorder_kernel(dslots L, dframe F, uint32_t tiles_all, uint32_t groups,
-                                                           uint32_t group)
-{
-    if (L.stop && *L.stop) return;   // a guarded round past the frame's target
-    const uint32_t tile = pt_tile_group_tile(tiles_all, groups, group, blockIdx.x);
-    const uint32_t p = tile * 256 + threadIdx.x;
-    const uint32_t s = tile * 256 + L.slotof[p];
-    const float4 r = L.ray[p];
-    uint32_t x, y;
-    const uint32_t key = TileOrderKey(SlotPixel(F, s, x, y), UnpackUnitVector(__float_as_uint(r.w)));
-    __syncthreads();
-    TileOrderStoreKeyed(L, s, key, r, threadIdx.x);
 }
 
 // Ray sources of the extend kernel: the renderer's slots, or the arrays of
@@ -1162,28 +1139,7 @@ PT_DEV void ExtendRay(const dscene& S, const Src& src, tstack<SPILL, CAP, E>& st
         LaneBegin(S, Ln, O, V, D);
         no_stats ns;
         if (S.g.ShapeCount != 0) {
-#if PT_WAVE_PRIO
-            // A wave still traversing after 32 / 64 / 96 steps raises its
-            // issue priority: the SIMD's arbiter then serves the long waves
-            // that set the launch's end before the short ones beside them.
-            uint32_t it = 0;
-            while (!LaneStep<SPILL, CAP, Src, no_stats, true, E>(S, Ln, st, src, slot, ns)) {
-                if ((++it & 31u) == 0) {
-                    uint32_t u = __builtin_amdgcn_readfirstlane(it);
-                    if (u == 32) __builtin_amdgcn_s_setprio(1);
-                    else if (u == 64) __builtin_amdgcn_s_setprio(2);
-                    else if (u == 96) __builtin_amdgcn_s_setprio(3);
-                }
-            }
-#elif PT_EXP_STEP_CAP
-            // Experiment only (not bit-exact): traversal cut after
-            // PT_EXP_STEP_CAP steps, to measure what the longest rays cost.
-            uint32_t it = 0;
-            while (!LaneStep<SPILL, CAP, Src, no_stats, true, E>(S, Ln, st, src, slot, ns) && ++it < PT_EXP_STEP_CAP) {}
-            if (Ln.Shape == 0xFFFFFFFEu) Ln.Shape = Ln.blas;   // cut inside a BLAS: its instance
-#else
             while (!LaneStep<SPILL, CAP, Src, no_stats, true, E>(S, Ln, st, src, slot, ns)) {}
-#endif
         }
         src.store(slot, Ln, S.vidx21 != 0);
         if (Ln.Shape == SHAPE_INDEX_NONE) {
@@ -1922,11 +1878,8 @@ __global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void round_kernel(
 // and new rays (shade -> next extend, TileOrder positions) visible to the
 // block's other waves.  The block's whole time is the tile's cost for the
 // next batch's longest-first order.
-#ifndef PT_ROUNDS_MINW
-#define PT_ROUNDS_MINW 0
-#endif
 template <uint32_t MATS, int CAP, class E>
-__global__ __launch_bounds__(256, PT_ROUNDS_MINW ? PT_ROUNDS_MINW : ShadeMinWaves<MATS>()) void rounds_kernel(
+__global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void rounds_kernel(
     dscene S, dslots L, dframe F, dparams Pm)
 {
     __shared__ E smem[CAP * 256];
@@ -2318,15 +2271,6 @@ static void LaunchShadeQ(const ptd::dscene& S, const ptd::dslots& L, const ptd::
     else
         hipLaunchKernelGGL((ptd::shade_classq_kernel<PT_MATS_ALL | PT_MATS_SCENE, COMPACT>), dim3(blocks), dim3(256), 0,
                            st, S, L, F, P, counts, list, capk);
-}
-
-hipError_t pt_launch_tile_reorder(const ptd::dslots& L, const ptd::dframe& F, uint32_t tiles_all, uint32_t groups,
-                                  uint32_t group, hipStream_t st)
-{
-    if (L.n == 0 || L.tile_count == 0) return hipSuccess;
-    hipLaunchKernelGGL(ptd::tile_reorder_kernel, dim3(L.tile_count), dim3(256), 0, st, L, F,
-                       tiles_all ? tiles_all : L.tile_count, groups, group);
-    return hipGetLastError();
 }
 
 bool pt_class_lists_supported(uint32_t scene_mats)

@@ -36,10 +36,6 @@ struct dslots {
     const uint32_t* stop = nullptr;   // guarded rounds (ptRenderFrame's last rounds): set -> the launch returns
     uint32_t n;
     uint32_t tile_count;    // n / 256: one block per tile
-#if PT_DSLOTS_PAD
-    uint32_t* pad_[3] = {};  // A/B builds: the kernel-argument layout of the class-list experiment build
-    uint32_t pad_n_ = 0;
-#endif
 };
 
 struct dframe {
@@ -128,12 +124,6 @@ hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd
 constexpr uint32_t CQ_SUB = 1;
 inline uint32_t pt_classq_sub_capacity(uint32_t tiles) { return (tiles + CQ_SUB - 1) / CQ_SUB * 256; }
 bool pt_class_lists_supported(uint32_t scene_mats);
-// TileOrder of a tile group's new rays after a class-pure shade.
-hipError_t pt_launch_tile_reorder(const ptd::dslots& L, const ptd::dframe& F, uint32_t tiles_all, uint32_t groups,
-                                  uint32_t group, hipStream_t st);
-#ifndef PT_LIST_REORDER
-#define PT_LIST_REORDER 0   // A/B builds: 1 = re-sort the rays by octant after each class-pure shade
-#endif
 hipError_t pt_launch_shade_classq(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F,
                                   const ptd::dparams& P, uint32_t scene_mats, bool compact, uint32_t* counts,
                                   uint32_t* next_counts, uint32_t* list, hipStream_t st, uint32_t tiles_all = 0,
@@ -143,21 +133,14 @@ hipError_t pt_launch_vertex_decode(const uint2* v, uint32_t n, float4* attr, flo
 // (pt_tile_group_count of them) and the dispatch-order segment starting at
 // pt_tile_group_start.  pt_launch_tile_order sorts one group's segment
 // longest-first (groups = 1: the whole frame).
-#ifndef PT_SPLIT_CONTIG
-#define PT_SPLIT_CONTIG 0   // experiment builds: 1 = group g owns the g-th contiguous run of tiles
-#endif
 __host__ __device__ inline uint32_t pt_tile_group_count(uint32_t tiles, uint32_t groups, uint32_t group)
 {
-    if (PT_SPLIT_CONTIG) {
-        const uint32_t chunk = (tiles + groups - 1) / groups, first = group * chunk;
-        return first < tiles ? (tiles - first < chunk ? tiles - first : chunk) : 0u;
-    }
     return group < tiles ? (tiles - group + groups - 1) / groups : 0u;
 }
 // The i-th tile of a group.
 __host__ __device__ inline uint32_t pt_tile_group_tile(uint32_t tiles, uint32_t groups, uint32_t group, uint32_t i)
 {
-    return PT_SPLIT_CONTIG ? group * ((tiles + groups - 1) / groups) + i : group + i * groups;
+    return group + i * groups;
 }
 __host__ __device__ inline uint32_t pt_tile_group_start(uint32_t tiles, uint32_t groups, uint32_t group)
 {

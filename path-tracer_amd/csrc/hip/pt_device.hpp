@@ -159,11 +159,9 @@ PT_DEV float FastRcp(float d)
     return __builtin_fmaf(e, y, y);
 }
 
-// Traversal use (PT_FAST_RCP, traverse.hpp) is off: it measured 1 % slower
-// on C3 extend than the IEEE division sequence (tools/gpu_ab.sh).
-#ifndef PT_FAST_RCP
-#define PT_FAST_RCP 0
-#endif
+// Not used by the traversal: it measured 1 % slower on C3 extend than the
+// IEEE division sequence (round 2); ptCheckFastReciprocal keeps
+// its bit-equality checked.
 
 PT_DEV bool FastRcpRange(float d)
 {

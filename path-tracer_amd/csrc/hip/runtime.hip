@@ -1125,6 +1125,13 @@ static uint32_t ShadeMats(const pt_basic_renderer* r)
     return m | PT_MATS_SCATTER;
 }
 
+// Whether the live paths take the grey record form.  Decided on the shade
+// instantiation's mask (pt_shade_mats), the same mask ShadeSlot tests as MATS:
+// a scene mask without glass can still map to an instantiation that has it
+// (diffuse + metal + fog -> PT_MATS_ALL), and that kernel reads the
+// four-float record.
+static bool GreyForm(const pt_basic_renderer* r) { return pt_grey_mats(pt_shade_mats(ShadeMats(r))); }
+
 // The record form of the renderer's live paths (GreyRecord, kernels.hip
 // StorePathVertex): grey while the shade mask keeps every Probability
 // wavelength-uniform and every active-shape stack empty.  A mask change
@@ -1135,7 +1142,7 @@ static uint32_t ShadeMats(const pt_basic_renderer* r)
 // stays in the four-float form until the next Reset or state write.
 static int SyncRecordForm(pt_device* d, pt_basic_renderer* r)
 {
-    const bool want = pt_grey_mats(ShadeMats(r));
+    const bool want = GreyForm(r);
     if (want != r->grey && r->slots.n) {
         const ptd::dframe F = Frame(r);
         if (!want) {
@@ -1166,7 +1173,7 @@ int ptResetBasicRenderer(pt_device* d, pt_basic_renderer* r)
     if (CheckReady(r) != 0) return -1;
     PT_HIP(hipSetDevice(d->id));
     // Every live path is replaced: the record form follows the shade mask.
-    r->grey = pt_grey_mats(ShadeMats(r));
+    r->grey = GreyForm(r);
     r->grey_blocked = false;
     r->slots.prob1 = r->grey ? r->prob1.ptr : nullptr;
     event_pair ep{};
@@ -1207,19 +1214,38 @@ static bool RoundFused(const pt_basic_renderer* r, const ptd::dslots& g)
     return mode == 2 || g.tile_count <= cap;
 }
 
-// Class-list buffers sized for PT_MAX_SPLIT tile groups (per group: 2
-// parities x classes x CQ_SUB counters, classes x CQ_SUB sub-lists of a whole
-// frame's capacity) plus the counters of single-stream rounds (region
-// PT_MAX_SPLIT, kept zero by its own parity), allocated on first use, zeroed.
-static int ClassListBuffers(pt_basic_renderer* r)
+// Class-list region of one tile group of K: classes x CQ_SUB sub-lists of
+// the largest group's capacity (group g holds at most ceil(T / K) tiles).
+static size_t ClassListStride(uint32_t tiles, uint32_t K)
 {
-    if (r->cq_list.ptr) return 0;
+    return (size_t)ptd::PT_OUTCOME_CLASSES * CQ_SUB * pt_classq_sub_capacity((tiles + K - 1) / K);
+}
+
+// Class-list buffers: the counters of PT_MAX_SPLIT tile groups (2 parities x
+// classes x CQ_SUB each) plus those of single-stream rounds (region
+// PT_MAX_SPLIT, kept zero by its own parity), allocated on first use and
+// zeroed; the lists sized for the K groups in use (K regions of
+// ClassListStride) or for a single-stream round over every tile, whichever
+// is larger (about 20 B per slot), grown when K grows.  A growth waits for
+// the device stream: the old lists may still be read by queued launches.
+static int ClassListBuffers(pt_device* d, pt_basic_renderer* r, uint32_t K)
+{
     const size_t nc = (size_t)ptd::PT_OUTCOME_CLASSES * CQ_SUB;
-    if (r->cq_counts.alloc((PT_MAX_SPLIT + 1) * 2 * nc) != hipSuccess ||
-        r->cq_list.alloc(PT_MAX_SPLIT * nc * pt_classq_sub_capacity(r->slots.tile_count)) != hipSuccess ||
-        hipMemset(r->cq_counts.ptr, 0, (PT_MAX_SPLIT + 1) * 2 * nc * sizeof(uint32_t)) != hipSuccess) {
-        SetError("class list allocation failed");
-        return -1;
+    const uint32_t T = r->slots.tile_count;
+    if (!r->cq_counts.ptr) {
+        if (r->cq_counts.alloc((PT_MAX_SPLIT + 1) * 2 * nc) != hipSuccess ||
+            hipMemset(r->cq_counts.ptr, 0, (PT_MAX_SPLIT + 1) * 2 * nc * sizeof(uint32_t)) != hipSuccess) {
+            SetError("class list allocation failed");
+            return -1;
+        }
+    }
+    const size_t need = std::max(ClassListStride(T, 1), K * ClassListStride(T, K));
+    if (need > r->cq_list.count) {
+        if (r->cq_list.ptr) PT_WAIT(d);
+        if (r->cq_list.alloc(need) != hipSuccess) {
+            SetError("class list allocation failed");
+            return -1;
+        }
     }
     return 0;
 }
@@ -1236,16 +1262,14 @@ static bool ClassListRounds(const pt_basic_renderer* r);
 static int ClassListShade(pt_device* d, pt_basic_renderer* r, const ptd::dslots& L, const ptd::dframe& F,
                           const ptd::dparams& P, hipStream_t st)
 {
-    if (int e = ClassListBuffers(r)) return e;
+    if (int e = ClassListBuffers(d, r, 1)) return e;
     const size_t nc = (size_t)ptd::PT_OUTCOME_CLASSES * CQ_SUB;
     uint32_t* cnt = r->cq_counts.ptr + PT_MAX_SPLIT * 2 * nc;
     uint32_t* cq = cnt + nc * r->cq_parity;
     uint32_t* cq_next = cnt + nc * (r->cq_parity ^ 1u);
     r->cq_parity ^= 1u;
-    (void)d;
     PT_HIP(pt_launch_shade_classq(r->scene->d, L, F, P, ShadeMats(r), ShadeCompact(r), cq, cq_next, r->cq_list.ptr,
                                   st));
-    if (PT_LIST_REORDER) PT_HIP(pt_launch_tile_reorder(L, F, 0, 1, 0, st));
     return 0;
 }
 
@@ -1350,17 +1374,7 @@ static int EnsureGroupStreams(pt_device* d, uint32_t K)
 {
     if (!d->fork_event) PT_HIP(hipEventCreateWithFlags(&d->fork_event, hipEventDisableTiming));
     for (uint32_t g = 0; g + 1 < K; g++) {
-#if PT_SPLIT_PRIO
-        // Experiment builds: group streams at the lowest (1) or highest (2) priority.
-        if (!d->group_stream[g]) {
-            int least = 0, greatest = 0;
-            PT_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-            PT_HIP(hipStreamCreateWithPriority(&d->group_stream[g], hipStreamNonBlocking,
-                                               PT_SPLIT_PRIO == 1 ? least : greatest));
-        }
-#else
         if (!d->group_stream[g]) PT_HIP(hipStreamCreateWithFlags(&d->group_stream[g], hipStreamNonBlocking));
-#endif
         if (!d->join_event[g]) PT_HIP(hipEventCreateWithFlags(&d->join_event[g], hipEventDisableTiming));
     }
     return 0;
@@ -1391,18 +1405,13 @@ static int RunRoundsSplit(pt_device* d, pt_basic_renderer* r, uint64_t k, uint32
     const bool lists = ClassLists(r);
     if (lists) {
         // Per group: 2 parities x classes counters (zero at the batch
-        // start) and a list region of classes x a whole frame's slots.
-        if (int e = ClassListBuffers(r)) return e;
+        // start) and a list region of ClassListStride words.
+        if (int e = ClassListBuffers(d, r, K)) return e;
         PT_HIP(hipMemsetAsync(r->cq_counts.ptr, 0, PT_MAX_SPLIT * 2 * ptd::PT_OUTCOME_CLASSES * CQ_SUB * sizeof(uint32_t),
                               d->stream));
     }
     PT_HIP(hipEventRecord(d->fork_event, d->stream));
     for (uint32_t g = 1; g < K; g++) PT_HIP(hipStreamWaitEvent(S[g], d->fork_event, 0));
-#if PT_SPLIT_STAGGER
-    static hipEvent_t stagger[PT_MAX_SPLIT - 1] = {};
-    for (uint32_t g = 0; g + 1 < K; g++)
-        if (!stagger[g]) PT_HIP(hipEventCreateWithFlags(&stagger[g], hipEventDisableTiming));
-#endif
     auto rounds = [&]() -> int {
         for (uint64_t i = 0; i < k; i++) {
             r->params.FrameIndex += 1;
@@ -1413,15 +1422,7 @@ static int RunRoundsSplit(pt_device* d, pt_basic_renderer* r, uint64_t k, uint32
                 event_pair ep{};
                 if (g == 0)
                     if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled)) return e;
-#if PT_SPLIT_STAGGER
-                // Experiment builds: group g's first extend starts after group
-                // g - 1's (the groups begin the batch a launch apart).
-                if (i == 0 && g > 0) PT_HIP(hipStreamWaitEvent(S[g], stagger[g - 1], 0));
-#endif
                 PT_HIP(pt_launch_extend(r->scene->d, G[g], F, r->slots.spill, S[g]));
-#if PT_SPLIT_STAGGER
-                if (i == 0 && g + 1 < K) PT_HIP(hipEventRecord(stagger[g], S[g]));
-#endif
                 if (g == 0) {
                     if (int e = EndTimed(d, ep)) return e;
                     if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled)) return e;
@@ -1430,12 +1431,11 @@ static int RunRoundsSplit(pt_device* d, pt_basic_renderer* r, uint64_t k, uint32
                     // Class-pure shade: the group's own counters (parity per
                     // round) and list region.
                     const size_t nc = (size_t)ptd::PT_OUTCOME_CLASSES * CQ_SUB;
-                    const size_t capk = pt_classq_sub_capacity(r->slots.tile_count);
                     uint32_t* cnt = r->cq_counts.ptr + g * 2 * nc;
                     PT_HIP(pt_launch_shade_classq(r->scene->d, G[g], F, P, mats, compact, cnt + nc * (i & 1u),
-                                                  cnt + nc * ((i & 1u) ^ 1u), r->cq_list.ptr + g * nc * capk, S[g],
+                                                  cnt + nc * ((i & 1u) ^ 1u),
+                                                  r->cq_list.ptr + g * ClassListStride(r->slots.tile_count, K), S[g],
                                                   r->slots.tile_count, K, g));
-                    if (PT_LIST_REORDER) PT_HIP(pt_launch_tile_reorder(G[g], F, r->slots.tile_count, K, g, S[g]));
                 } else {
                     PT_HIP(pt_launch_shade(r->scene->d, G[g], F, P, mats, compact, S[g]));
                 }
@@ -1636,27 +1636,27 @@ static int RunGuardedRounds(pt_device* d, pt_basic_renderer* r, uint32_t n, uint
 }
 
 constexpr double GUARD_PREDICTED = 8.0;   // rounds left, by the last batch's rate, for the guarded end
-#ifndef PT_FRAME_GUARD
-#define PT_FRAME_GUARD 1   // A/B builds: 0 = round 4's read-back after every batch
-#endif
 
 // Benchmark-mode frame: Reset, Run(2) as after a restart
 // (application.cpp:109-110), then Run(1) rounds -- one new seed each, as the
 // application's frame loop issues them (application.cpp:100-115,
 // basic.cpp:306-332) -- until the paths completed since the Reset reach
 // target_samples (the accumulator's alpha sum) or max_rounds rounds ran.
-// The completed count is read back between batches of rounds: a batch is
-// never longer than the rounds that could not reach the target even if every
-// slot completed a path each round, or than 90 % of the rounds the last
-// batch's completion rate predicts, and within the last 16 predicted rounds
-// only the former.  The first batch after Run(2) needs no read-back (at most
-// 2 px paths completed so far), and the last rounds (at most GUARD_PREDICTED
-// by the rate) run guarded: a device-side check before each round stops the
-// rest once the target is reached, so they need one read-back in all.  So the frame ends at the reference's round (the first
-// whose total reaches the target) unless the completion rate rises by more
-// than 1/0.9 - 1 = 11 % within one rate-sized batch; the rate of a frame
-// past its first rounds moves by well under 1 % per batch (the C3 1024-spp
-// frame ends at the reference's round: tests/test_gpu_coverage.py).
+//
+// The frame ends at the reference's round -- the first whose total reaches
+// the target -- unconditionally.  A round completes at most one path per
+// owned pixel (px), so with `remaining` paths to go the first
+// ceil(remaining / px) - 1 rounds cannot reach the target: every batch of
+// rounds enqueued without a look at the count is at most ceil(remaining /
+// px) long, its last round the first that may reach it.  The count is read
+// back between batches.  When the last batch's completion rate says at most
+// GUARD_PREDICTED rounds are left, the rounds run guarded instead: a device
+// check before each round returns the round's launches at once when the
+// target is already reached (RunGuardedRounds), so a rate that changes can
+// cost a read-back but never a round.  The rate decides only how the rounds
+// are issued, never how many run.  Measured on the C3 1024-spp frame
+// (tools/exp_frame_end.py, profiles/r06_frame_end): 16 batches, +2 ms
+// (0.19 %) against the same 2 760 rounds in one call with no read-back.
 int ptRenderFrame(pt_device* d, pt_basic_renderer* r, uint64_t target_samples, uint32_t max_rounds,
                   uint32_t* rounds_out, uint64_t* samples_out)
 {
@@ -1668,10 +1668,9 @@ int ptRenderFrame(pt_device* d, pt_basic_renderer* r, uint64_t target_samples, u
     uint64_t samples = 0, prev = 0;
     uint32_t last_batch = 0;
     const uint64_t px = std::max<uint64_t>(r->valid_slots, 1);   // paths one round can complete
-    // Every round completes at most px paths, so the two rounds of Run(2)
-    // leave at least target - 2 px to go: that many rounds' worth runs
-    // before the first read-back.
-    if (PT_FRAME_GUARD && target_samples > 2 * px) {
+    // The two rounds of Run(2) complete at most 2 px paths: the first batch
+    // needs no read-back.
+    if (target_samples > 2 * px) {
         const uint64_t k = std::min<uint64_t>((target_samples - 2 * px + px - 1) / px, max_rounds - rounds);
         if (k >= 1) {
             if (int e = RunRounds(d, r, k)) return e;
@@ -1682,21 +1681,12 @@ int ptRenderFrame(pt_device* d, pt_basic_renderer* r, uint64_t target_samples, u
     for (;;) {
         if (int e = ptGetStats(d, r, nullptr, &samples)) return e;
         if (samples >= target_samples || rounds >= max_rounds) break;
-        uint64_t remaining = target_samples - samples;
-        uint64_t k = (remaining + px - 1) / px;                      // cannot overshoot
+        const uint64_t remaining = target_samples - samples;
         if (last_batch > 0 && samples > prev) {
-            double rate = (double)(samples - prev) / last_batch;     // completions per round
-            // 90 % of the rounds the last batch's rate predicts; within the
-            // last 16 predicted rounds only the rounds that cannot overshoot,
-            // so a rate that rises near the end cannot carry the frame past
-            // the round that first reaches the target.
+            const double rate = (double)(samples - prev) / last_batch;   // completions per round
             const double predicted = (double)remaining / rate;
-            const uint64_t kr = (uint64_t)(0.9 * predicted);
-            if (kr >= 16) k = std::max<uint64_t>(k, kr);
-            // The last few rounds: guarded, enqueued together with one
-            // read-back after them instead of one per batch (C1's 24-round
-            // frame took five read-backs).
-            if (PT_FRAME_GUARD && predicted <= GUARD_PREDICTED) {
+            if (predicted <= GUARD_PREDICTED) {
+                // The last few rounds: guarded, with one read-back after them.
                 const uint32_t n = (uint32_t)std::min<uint64_t>((uint64_t)(1.25 * predicted) + 2, max_rounds - rounds);
                 if (n >= 2) {
                     uint32_t ran = 0;
@@ -1708,7 +1698,7 @@ int ptRenderFrame(pt_device* d, pt_basic_renderer* r, uint64_t target_samples, u
                 }
             }
         }
-        k = std::max<uint64_t>(1, std::min<uint64_t>(k, max_rounds - rounds));
+        const uint64_t k = std::min<uint64_t>((remaining + px - 1) / px, max_rounds - rounds);   // cannot overshoot
         if (int e = RunRounds(d, r, k)) return e;
         rounds += (uint32_t)k;
         prev = samples;

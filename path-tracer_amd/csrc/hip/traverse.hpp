@@ -12,19 +12,6 @@ namespace ptd {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 PT_DEV float4 F4(f32x4 v) { return make_float4(v.x, v.y, v.z, v.w); }
 
-// PT_STEP_JOIN: LaneStep's BLAS part as divergent compute + joined state
-// update (below); 0 = the branch-local updates.
-#ifndef PT_STEP_JOIN
-#define PT_STEP_JOIN 1
-#endif
-// PT_TWO_LEVEL: a BLAS internal step also takes the next level when the
-// child it continues with is internal (LaneStep).  Measured neutral (C3
-// extend 0.330 vs 0.330 ms, rank-of-8 round 0.112 vs 0.112, C5 -2 %), and
-// with a 256-byte record per pair holding both children's pairs (the
-// second level an L1 hit half the time) C3 3 % slower: off.
-#ifndef PT_TWO_LEVEL
-#define PT_TWO_LEVEL 0
-#endif
 
 // --- traversal stack: LDS columns + global spill ----------------------------
 
@@ -79,12 +66,7 @@ PT_DEV void SetLevelRay(const dscene& S, lane_state& L, pt3 O, pt3 V)
     L.O = O;
     L.V = V;
     L.exact = S.fast_div && FastDivRay(O, V);
-#if PT_FAST_RCP
-    L.Y = v3(FastRcp(V.x), FastRcp(V.y), FastRcp(V.z));
-    if (!(FastRcpRange(V.x) & FastRcpRange(V.y) & FastRcpRange(V.z))) L.Y = v3(1.0f / V.x, 1.0f / V.y, 1.0f / V.z);
-#else
     L.Y = v3(1.0f / V.x, 1.0f / V.y, 1.0f / V.z);
-#endif
 }
 
 PT_DEV void LaneBegin(const dscene& S, lane_state& L, pt3 O, pt3 V, float Duration)
@@ -203,13 +185,7 @@ PT_DEV bool FaceTest(const dscene& S, uint32_t F, const lane_state& L, bool vali
     // single select.
     pt3 RCE2 = cross(L.V, Edge2);
     float Det = dot(Edge1, RCE2);
-#if PT_FAST_RCP
-    // FastRcp == 1.0f / Det bit for bit in its range (pt_device.hpp).
-    float InvDet = FastRcp(Det);
-    if (!FastRcpRange(Det)) InvDet = 1.0f / Det;
-#else
     float InvDet = 1.0f / Det;
-#endif
     pt3 Sv = L.O - P0;
     U = InvDet * dot(Sv, RCE2);
     pt3 SCE1 = cross(Sv, Edge1);
@@ -452,7 +428,6 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP, SE>& st,
 {
     ss.step();
     bool tlas = L.blas == SHAPE_INDEX_NONE;
-#if PT_STEP_JOIN
     if (FACE_STEP && !tlas) {
         // The divergent part of a BLAS step computes only fresh values (face:
         // miss flag, T, U, W; internal node: TA, TB and the child words); every
@@ -494,29 +469,6 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP, SE>& st,
             IntersectBoxPair(L.O, L.V, L.Y, L.Time, a0, a1, b0, b1, L.exact, TA, TB);
             aw0 = __float_as_uint(a0.w), aw1 = __float_as_uint(a1.w);
             bw0 = __float_as_uint(b0.w), bw1 = __float_as_uint(b1.w);
-#if PT_TWO_LEVEL
-            // Two levels per step: when the child the reference continues
-            // with is itself internal, its own child pair is tested in this
-            // step too -- the reference's next loop iteration, with the same
-            // Hit.Time (no face is tested in between).  The first level's
-            // set-aside child is pushed first, then the join applies the
-            // second level's decision.  Same pushes, pops and order.
-            bool g1 = TA > TB;
-            uint32_t nw0 = g1 ? bw0 : aw0, nw1 = g1 ? bw1 : aw1;
-            if ((g1 | (TA < PT_INFINITY)) & (nw1 == 0)) {
-                float Tf = g1 ? TA : TB;
-                if ((Tf < PT_INFINITY) & (L.dB < 32))
-                    st.put(L.dT + L.dB++, BlasPush<SE>(S, g1 ? aw0 : bw0, g1 ? aw1 : bw1, L.na + (g1 ? 0u : 1u)));
-                ss.node(true);
-                ss.internal();
-                pair = nw0;
-                const float4* Cp = S.mesh_nodes + 2 * (size_t)nw0;
-                float4 c0 = Cp[0], c1 = Cp[1], c2 = Cp[2], c3 = Cp[3];
-                IntersectBoxPair(L.O, L.V, L.Y, L.Time, c0, c1, c2, c3, L.exact, TA, TB);
-                aw0 = __float_as_uint(c0.w), aw1 = __float_as_uint(c1.w);
-                bw0 = __float_as_uint(c2.w), bw1 = __float_as_uint(c3.w);
-            }
-#endif
         }
         L.Time = fmiss ? L.Time : fT;
         L.Shape = fmiss ? L.Shape : 0xFFFFFFFEu;
@@ -551,7 +503,6 @@ PT_DEV bool LaneStep(const dscene& S, lane_state& L, tstack<SPILL, CAP, SE>& st,
         if (!tlas) return false;
         return TlasStep(S, L, st, src, slot, ss);
     }
-#endif
     if (!tlas) {
         bool moved = false;
         if (L.nb > 0) {

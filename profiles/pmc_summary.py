@@ -17,13 +17,20 @@ import sys
 def load(path):
     per = collections.defaultdict(float)
     names = {}
+    span = {}
     for r in csv.DictReader(open(path)):
         key = (r["Dispatch_Id"], r["Counter_Name"])
         per[key] += float(r["Counter_Value"])
         names[r["Dispatch_Id"]] = r["Kernel_Name"]
+        if r.get("Start_Timestamp") and r.get("End_Timestamp"):
+            span[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for (d, c), v in per.items():
         agg[names[d]][c].append(v)
+    # The profiled dispatches' own durations (rocprofv3 serialises them):
+    # the time the counters of the same dispatches accrued in.
+    for d, ns in span.items():
+        agg[names[d]]["dispatch_ns"].append(float(ns))
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in agg.items()}
 
 
@@ -45,7 +52,7 @@ def main():
     # bench.py's shade time (both launches) meets its bytes.
     if "class_list" in kernels and "shade_classq" in kernels and "shade" not in kernels:
         a, b = kernels["class_list"], kernels["shade_classq"]
-        kernels["shade"] = {c: a.get(c, 0.0) + b[c] for c in b}
+        kernels["shade"] = {c: a.get(c, 0.0) + b[c] for c in b}   # dispatch_ns too: the pair's time
     result = {}
     for k, d in kernels.items():
         e = {c: round(v, 1) for c, v in d.items()}
@@ -63,6 +70,12 @@ def main():
             e["valu_issue_frac"] = round(d["SQ_INSTS_VALU"] * 2 / (1024 * max(cycles, 1)), 4)
         if "SQ_THREAD_CYCLES_VALU" in d and "SQ_ACTIVE_INST_VALU" in d:
             e["valu_active_lanes"] = round(d["SQ_THREAD_CYCLES_VALU"] / max(d["SQ_ACTIVE_INST_VALU"], 1), 1)
+        if "dispatch_ns" in d:
+            e["dispatch_ms"] = round(d["dispatch_ns"] * 1e-6, 5)
+            if "hbm_bytes" in e:
+                # HBM GB/s of the profiled (serialised) dispatches: bytes and
+                # time from the same dispatches.
+                e["hbm_gbps_serialised"] = round(e["hbm_bytes"] / d["dispatch_ns"], 2)
         if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d:
             e["l2_hit_rate"] = round(d["TCC_HIT_sum"] / max(d["TCC_HIT_sum"] + d["TCC_MISS_sum"], 1), 4)
         result[k] = e

@@ -67,7 +67,7 @@ class PatchedPacks:
         return self._p
 
 
-def render_and_check(pt, dev, source, W=128, H=72, schedule=(2, 1, 1)):
+def render_and_check(pt, dev, source, W=128, H=72, schedule=(2, 1, 1), termination=0.0):
     ds = pt.DeviceScene(dev)
     ds.update(source)
     sb = pt.SampleBuffer(dev, W, H)
@@ -75,6 +75,7 @@ def render_and_check(pt, dev, source, W=128, H=72, schedule=(2, 1, 1)):
     o = oracle_lib.OracleRenderer(source.packs(), W, H)
     for x in (r, o):
         x.RenderFlags = 3
+        x.PathTerminationProbability = termination
         x.reset()
     info = r.shade_info()
     for x in (r, o):
@@ -163,6 +164,38 @@ def test_lean_scene_plus_one_shape(pt, dev, material):
     assert info["scene_mask"] & want and info["kernel_mask"] & want
     assert info["grey_records"] == (material == "metal")
     s.close()
+
+
+@pytest.mark.parametrize("config,metal", [(1, False), (3, False), (3, True)])
+def test_fog_without_glass_keeps_four_float_records(pt, dev, config, metal):
+    """SceneScatterRate > 0 in a scene with no glass: the
+    scene mask (diffuse [+ metal] + scatter) has no translucent bit, but the
+    shade instantiation it maps to (PT_MATS_ALL) does and reads the four-float
+    record, so the renderer must not take the grey form.  Bit-exact against
+    the oracle on the accumulator and on every read_state field, Probability
+    included.  In fog that fills the scene no path escapes (a ray to the sky
+    always scatters first), so roulette (termination 0.2) ends paths and new
+    ones start from the camera."""
+    s = scene_for(pt, config)
+    owned = None
+    if metal:
+        owned = s = pt.Scene.config(config)
+        m = s.create_material(pt.MATERIAL_BASIC_METAL, "Brass", BaseColor=(0.9, 0.7, 0.3), Roughness=0.2)
+        cam = s.arrays()["cameras"][0]["Transform"]["To"].reshape(4, 4).T
+        eye, fwd = cam[:3, 3], -cam[:3, 2]
+        s.create_entity(pt.ENTITY_SPHERE, position=tuple(eye + 1.5 * fwd), scale=(0.6, 0.6, 0.6), material=m)
+        s.pack()
+
+    def edit(g):
+        g["SceneScatterRate"] = np.float32(0.35)
+    src = PatchedPacks(pt, s, globals_edit=edit)
+    info = render_and_check(pt, dev, src, schedule=(2, 1, 1, 1), termination=0.2)
+    assert info["scene_mask"] & pt.SHADE_SCATTER
+    assert not info["scene_mask"] & pt.SHADE_TRANSLUCENT
+    assert info["kernel_mask"] & pt.SHADE_TRANSLUCENT
+    assert not info["grey_records"]
+    if owned is not None:
+        owned.close()
 
 
 @pytest.mark.parametrize("config,grey", [(1, True), (2, False), (5, False)])

@@ -1,110 +1,78 @@
 """Thread scaling of the CPU baseline (the oracle: scalar C++ restatement of
-the integrator, std::thread over pixels) on the C3 frame, 1..T threads, over
-SETTLED rounds: one oracle is reset, run through Run(2) + `settle` rounds at
-the largest thread count (the path population past its first rounds, where
-the per-round cost is stationary), then each thread count times `rounds`
-consecutive rounds of the same render (oracle_set_threads between them).
+the integrator, std::thread over pixels) on the C3 frame, 1..T threads.
 
-VERDICT r04 #6: round 4 timed 2 rounds right after Reset (the shortest paths)
-per thread count.  Each thread count runs pinned to that many distinct
-physical cores of one package (bench.pick_cores), as bench.py's cpu_baseline
-does.  On the GPU box a job's CPU share is 16 threads
-(OMP_NUM_THREADS) of a 256-CPU host shared with the other GPUs' jobs; this
-tool stays inside that share, and states the all-core figure as an
-extrapolation of the measured per-thread rate, not a measurement.
+One code path with bench.py's CPU leg: bench.settled_oracle
+(Reset, Run(2), 34 settle rounds) and bench.time_oracle_rounds (threads
+pinned to distinct physical cores of one package, at least 32 rounds, more
+while under 15 s).  The table's first row IS the bench leg: a fresh oracle at
+the job's thread count, settled and timed exactly as bench.py times it.  The
+other thread counts then time the rounds that follow on the same render
+(oracle_set_threads), largest first.
 
-usage: python tools/cpu_scaling.py OUT.json [--threads 1,2,4,8,16] [--settle 34] [--rounds 32]
+On the GPU box a job's CPU share is 16 threads (OMP_NUM_THREADS) of a
+256-CPU host shared with the other GPUs' jobs; this tool stays inside that
+share, and states the all-core figure as an extrapolation of the measured
+per-thread rate, not a measurement.
+
+usage: python tools/cpu_scaling.py OUT.json [--threads 16,8,4,2,1] [--rounds 32] [--max-seconds 30]
 """
 import argparse
 import json
 import os
 import sys
-import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
-sys.path.insert(0, str(ROOT / "tests"))
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("out")
-    ap.add_argument("--threads", default="1,2,4,8,16")
-    ap.add_argument("--settle", type=int, default=34)
-    ap.add_argument("--rounds", type=int, default=32)
+    ap.add_argument("--threads", default="", help="comma list (default: the bench leg's count, then halvings to 1)")
+    ap.add_argument("--rounds", type=int, default=32, help="minimum timed rounds per thread count")
+    ap.add_argument("--max-seconds", type=float, default=30.0)
     ap.add_argument("--config", type=int, default=3)
-    ap.add_argument("--init-gpu", action="store_true",
-                    help="create a HIP device first, as bench.py's process has when it times its cpu_baseline")
     a = ap.parse_args()
     import bench
-    import oracle_lib  # test infrastructure: the CPU baseline, never the product path
     pt = bench.load_package()
-    dev = pt.Device(0) if a.init_gpu else None
     scene = pt.Scene.config(a.config)
     info = scene.info
-    counts = [int(x) for x in a.threads.split(",")]
-    o = oracle_lib.OracleRenderer(scene.packs(), info.width, info.height, threads=max(counts))
-    o.RenderFlags = info.render_flags
-    o.reset()
-    o.run(2)
-    t0 = time.perf_counter()
-    for _ in range(a.settle):
-        o.run(1)
-    settle_s = time.perf_counter() - t0
-    print(json.dumps({"settle_rounds": a.settle, "settle_s": round(settle_s, 2), "threads": max(counts)}), flush=True)
+    lead, allowed, omp = bench.cpu_threads()
+    if a.threads:
+        counts = [int(x) for x in a.threads.split(",")]
+    else:
+        counts, t = [lead], lead
+        while t > 1:
+            t //= 2
+            counts.append(t)
+    counts = sorted(set(counts), reverse=True)
+    o = bench.settled_oracle(scene, info.width, info.height, counts[0], 3)
     rows = []
-    home = os.sched_getaffinity(0)
-    allowed = len(home)
-    for t in counts:
-        o.set_threads(t)
-        # The same placement as bench.py's cpu_baseline: t threads pinned to
-        # t distinct, least busy physical cores of one package.
-        pinned, placement = bench.pick_cores(t) if t < allowed else (None, "every affinity CPU, unpinned")
-        os.sched_setaffinity(0, pinned if pinned else home)
-        r0, s0 = o.counters()
-        t0 = time.perf_counter()
-        c0 = time.process_time()
-        per_round = []
-        for _ in range(a.rounds):
-            t1 = time.perf_counter()
-            o.run(1)
-            per_round.append(time.perf_counter() - t1)
-        dt = time.perf_counter() - t0
-        cpu_s = time.process_time() - c0
-        r1, s1 = o.counters()
-        per_round.sort()
-        row = {"threads": t, "rounds": a.rounds, "seconds": round(dt, 3),
-               "mrays_per_s": round((r1 - r0) / dt / 1e6, 4),
-               "msamples_per_s": round((s1 - s0) / dt / 1e6, 4),
-               "median_round_s": round(per_round[len(per_round) // 2], 4),
-               "min_round_s": round(per_round[0], 4), "max_round_s": round(per_round[-1], 4),
-               "cpu_seconds": round(cpu_s, 2),
-               "mrays_per_cpu_s_x_threads": round((r1 - r0) / max(cpu_s, 1e-9) * t / 1e6, 4),
-               "placement": placement, "pinned_cpus": sorted(pinned) if pinned else None}
-        os.sched_setaffinity(0, home)
+    for i, t in enumerate(counts):
+        # The first row: bench.py's CPU leg exactly (fresh settled render,
+        # its round minimum and time bound); the smaller counts time fewer
+        # rounds when a round is slow (a 1-thread C3 round takes ~2.4 s).
+        mx = a.max_seconds if i == 0 else min(a.max_seconds, 20.0)
+        est = rows[0]["median_round_s"] * counts[0] / t if rows else 0.0   # this count's round, predicted
+        mn = a.rounds if i == 0 else max(4, min(a.rounds, int(mx / max(est, 1e-3))))
+        row = bench.time_oracle_rounds(o, t, mn, mx)
+        row["bench_leg"] = i == 0 and t == lead
         rows.append(row)
         print(json.dumps(row), flush=True)
     o.close()
-    if dev is not None:
-        dev.close()
-    base = rows[0]["mrays_per_s"] / rows[0]["threads"]
+    base = rows[-1]["mrays_per_s"] / rows[-1]["threads"]
     for r in rows:
-        r["efficiency_vs_1_thread"] = round(r["mrays_per_s"] / (base * r["threads"]), 3)
+        r["efficiency_vs_fewest_threads"] = round(r["mrays_per_s"] / (base * r["threads"]), 3)
     host = os.cpu_count() or 1
-    try:
-        aff = len(os.sched_getaffinity(0))
-    except OSError:
-        aff = host
-    last = rows[-1]
+    top = rows[0]
     out = {"config": f"C{a.config} {info.width}x{info.height}", "cpu_model": bench.cpu_model(), "host_cpus": host,
-           "affinity_cpus": aff, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
-           "hip_device_initialised": a.init_gpu,
-           "method": f"one render: Reset, Run(2), {a.settle} settle rounds at {max(counts)} threads, then "
-                     f"{a.rounds} timed consecutive rounds per thread count",
+           "affinity_cpus": allowed, "omp_num_threads": omp or None,
+           "method": f"bench.settled_oracle (Reset, Run(2), {bench.CPU_SETTLE_ROUNDS} settle rounds at {counts[0]} "
+                     "threads), then bench.time_oracle_rounds per thread count, largest first, on the same render",
            "rows": rows,
-           "extrapolated_all_host_cpus_mrays_per_s": round(last["mrays_per_s"] / last["threads"] * host, 1),
-           "extrapolation": f"{last['threads']}-thread rate per thread x {host} host CPUs (linear; not measured: "
+           "extrapolated_all_host_cpus_mrays_per_s": round(top["mrays_per_s"] / top["threads"] * host, 1),
+           "extrapolation": f"{top['threads']}-thread rate per thread x {host} host CPUs (linear; NOT measured: "
                             "the job's CPU share is its OMP_NUM_THREADS, the rest of the host belongs to the "
                             "other GPUs' jobs)"}
     Path(a.out).write_text(json.dumps(out, indent=1))

@@ -27,7 +27,9 @@ for k in ("extend", "raygen", "shade", "round", "rounds"):
     div = per_batch if k == "rounds" else 1    # per round
     entry["kernels"][k] = {x: int(s[k][x] / div) for x in ("hbm_bytes", "hbm_read_bytes", "hbm_write_bytes")
                            if x in s[k]}
-    iss = {x: s[k][x] for x in ("valu_issue_frac", "valu_active_lanes") if x in s[k]}
+    if "dispatch_ms" in s[k]:
+        entry["kernels"][k]["dispatch_ms"] = s[k]["dispatch_ms"] / div   # the profiled, serialised dispatch
+    iss = {x: s[k][x] for x in ("valu_issue_frac", "valu_active_lanes", "l2_hit_rate") if x in s[k]}
     for x in ("SQ_INSTS_VALU", "SQ_INSTS_SALU"):
         if x in s[k]:
             iss[x.lower()] = int(s[k][x] / div)
