@@ -311,9 +311,6 @@ def main():
                     help="tile groups on concurrent streams (ptSetBasicRendererSplit): 0 automatic, 1 off, K")
     ap.add_argument("--class-lists", type=int, default=0,
                     help="class-pure shade in tile groups (ptSetBasicRendererClassLists): 0 automatic, 1 off")
-    ap.add_argument("--extend-cap", type=int, default=0,
-                    help="step-capped extend with a compacted continuation (ptSetBasicRendererExtendCap): "
-                         "0 automatic, 1 off, S wave steps")
     ap.add_argument("--streams", type=int, default=0,
                     help="path streams per owned pixel (0: auto -- bands fill ~2^21 slots per launch, samples 1)")
     ap.add_argument("--inject-failure", type=int, default=-1, metavar="RANK",
@@ -382,11 +379,6 @@ def main():
         class_lists = r.class_lists()
     except AttributeError:   # an older library under PT_HIP_LIB (A/B builds)
         class_lists = None
-    try:
-        r.set_extend_cap(args.extend_cap)
-        extend_cap = r.extend_cap()
-    except AttributeError:   # an older library under PT_HIP_LIB (A/B builds)
-        extend_cap = None
     split = r.split()
     launch_slots = slots_owned * split["timed_tiles"] / max(split["tiles"], 1) if split["groups"] > 1 else slots_owned
     # This rank's frame target (Σ alpha): samples -> 1/N of spp x frame,
@@ -629,7 +621,6 @@ def main():
             "slots_per_launch_rank0": slots_owned,
             "split": split["groups"],
             "class_lists": class_lists,
-            "extend_cap": extend_cap,
             "frame_target_samples_rank0": target,
             "mesh_faces": info.mesh_face_count,
             "image_identity": identity,

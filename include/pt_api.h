@@ -268,16 +268,6 @@ int                ptGetBasicRendererClassLists(const pt_basic_renderer* rendere
 int                ptSetBasicRendererSplit(pt_basic_renderer* renderer, uint32_t groups);
 int                ptGetBasicRendererSplit(const pt_basic_renderer* renderer, uint32_t* groups, uint32_t* timed_tiles,
                                            uint32_t* tiles);
-/* Step-capped extend (no reference counterpart: a launch schedule).  Each
- * extend launch of the renderer's rounds stops every wave after `steps` wave
- * steps; the rays still traversing save their traversal state to a packed
- * queue, and a continuation launch traces them densely (compaction across
- * launches).  Results are identical.  steps: 0 = automatic (32, on scenes
- * whose traversal stack needs no spill rows), 1 = off, >= 2 = that many.
- * ptGetBasicRendererExtendCap sets *steps to the cap in use now (0 = off).
- * Default 0. */
-int                ptSetBasicRendererExtendCap(pt_basic_renderer* renderer, uint32_t steps);
-int                ptGetBasicRendererExtendCap(const pt_basic_renderer* renderer, uint32_t* steps);
 /* OpenPBR shading (opt-in extension, no reference counterpart): 0 (default)
  * = an OpenPBR hit ends its path with no contribution, as in the reference,
  * whose integrator does not compile its OpenPBR BSDF (scene.glsl.inc:685);

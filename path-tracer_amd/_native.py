@@ -259,8 +259,6 @@ HIP_API = {
     "ptRunBasicRendererRounds": (_i32, [_vp, _vp, _u32]),
     "ptSetBasicRendererRoundBatch": (_i32, [_vp, _u32]),
     "ptSetBasicRendererSplit": (_i32, [_vp, _u32]),
-    "ptSetBasicRendererExtendCap": (_i32, [_vp, _u32]),
-    "ptGetBasicRendererExtendCap": (_i32, [_vp, _u32ptr]),
     "ptSetBasicRendererClassLists": (_i32, [_vp, _u32]),
     "ptGetBasicRendererClassLists": (_i32, [_vp, _u32ptr]),
     "ptGetBasicRendererSplit": (_i32, [_vp, _u32ptr, _u32ptr, _u32ptr]),

@@ -1125,55 +1125,11 @@ constexpr bool kRendererSource = std::is_same<Src, ray_source_slots>::value;
 // then trace unrelated chunks, losing the L1 reuse of a tile's four waves,
 // and the dispatcher already balances the 8100 one-tile blocks.)
 //
-// The ShadeOrder outcome class of a traced ray: hit diffuse / metal /
-// translucent / other material, or miss (4); single-material scenes mark
-// misses only.
-PT_DEV uint32_t OutcomeClass(const dscene& S, const lane_state& Ln)
-{
-    if (Ln.Shape == SHAPE_INDEX_NONE) return 4u;
-    if (!S.mat_classes) return 0u;
-    uint32_t T = S.material[32 * (size_t)S.shapes[Ln.Shape].MaterialIndex];
-    return T == PT_MATERIAL_TYPE_BASIC_DIFFUSE ? 0u
-         : T == PT_MATERIAL_TYPE_BASIC_METAL ? 1u
-         : T == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT ? 2u : 3u;
-}
-
-// Compaction across launches: a lane of a capped extend still
-// traversing after Q.steps wave steps saves everything its next LaneStep
-// reads -- the current-level ray (its reciprocal and fast-division flag are
-// recomputed by SetLevelRay, as every level change sets them), the closest
-// hit so far, the node words, the level, both stack depths and the stack
-// entries -- at a packed queue index: one ballot over the wave's queued
-// lanes, one atomic by the lowest, and the lane's rank among them (mbcnt).
-template <bool SPILL, int CAP, class E>
-PT_DEV void ContSave(const dcont& Q, const lane_state& L, const tstack<SPILL, CAP, E>& st, uint32_t pos)
-{
-    const uint64_t m = __ballot(1);
-    const uint32_t lead = (uint32_t)__ffsll((long long)m) - 1u;
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    uint32_t base = 0;
-    if (rank == 0) base = atomicAdd(Q.count, (uint32_t)__popcll(m));
-    base = (uint32_t)__shfl((int)base, (int)lead, 64);
-    const uint32_t q = base + rank;
-    Q.pos[q] = pos;
-    Q.ot[q] = make_float4(L.O.x, L.O.y, L.O.z, L.Time);
-    Q.vs[q] = make_float4(L.V.x, L.V.y, L.V.z, __uint_as_float(L.Shape));
-    Q.cp[q] = make_float4(L.C.x, L.C.y, L.C.z, __uint_as_float(L.Prim));
-    Q.nd[q] = make_uint4(L.na, L.nb, L.blas, L.dT | (L.dB << 16));
-    Q.hh[q] = make_uint2(L.HA, L.HB);
-    E* stk = static_cast<E*>(Q.stack);
-    const uint32_t depth = L.dT + L.dB;
-    for (uint32_t i = 0; i < depth; i++) stk[(size_t)i * Q.cap + q] = (E)st.get(i);
-}
-
 // One ray: Trace() by LaneStep to completion, the compact hit stored, and
 // the ray's ShadeOrder outcome class ballotted (positions outside the image:
-// class 0, shade skips them).  CAPPED (the renderer's step-capped extend):
-// a lane not done after Q->steps steps is queued instead (ContSave); its
-// hit and its outcome bit come from the continuation.
-template <bool SPILL, int CAP, class E, class Src, bool CAPPED = false>
-PT_DEV void ExtendRay(const dscene& S, const Src& src, tstack<SPILL, CAP, E>& st, uint32_t slot,
-                      const dcont* Q = nullptr)
+// class 0, shade skips them).
+template <bool SPILL, int CAP, class E, class Src>
+PT_DEV void ExtendRay(const dscene& S, const Src& src, tstack<SPILL, CAP, E>& st, uint32_t slot)
 {
     pt3 O, V;
     float D;
@@ -1182,34 +1138,26 @@ PT_DEV void ExtendRay(const dscene& S, const Src& src, tstack<SPILL, CAP, E>& st
         lane_state Ln;
         LaneBegin(S, Ln, O, V, D);
         no_stats ns;
-        bool queued = false;
         if (S.g.ShapeCount != 0) {
-            if constexpr (CAPPED) {
-                uint32_t it = 0;
-                bool done;
-                while (!(done = LaneStep<SPILL, CAP, Src, no_stats, true, E>(S, Ln, st, src, slot, ns)) &&
-                       ++it < Q->steps) {}
-                queued = !done;
-            } else {
-                while (!LaneStep<SPILL, CAP, Src, no_stats, true, E>(S, Ln, st, src, slot, ns)) {}
-            }
+            while (!LaneStep<SPILL, CAP, Src, no_stats, true, E>(S, Ln, st, src, slot, ns)) {}
         }
-        if (queued) {
-            if constexpr (CAPPED) ContSave(*Q, Ln, st, slot);
-            cls = PT_OUTCOME_CLASSES;   // no class bit yet
-        } else {
-            src.store(slot, Ln, S.vidx21 != 0);
-            cls = OutcomeClass(S, Ln);
+        src.store(slot, Ln, S.vidx21 != 0);
+        if (Ln.Shape == SHAPE_INDEX_NONE) {
+            cls = 4;
+        } else if (S.mat_classes) {
+            uint32_t T = S.material[32 * (size_t)S.shapes[Ln.Shape].MaterialIndex];
+            cls = T == PT_MATERIAL_TYPE_BASIC_DIFFUSE ? 0u
+                : T == PT_MATERIAL_TYPE_BASIC_METAL ? 1u
+                : T == PT_MATERIAL_TYPE_BASIC_TRANSLUCENT ? 2u : 3u;
         }
     }
     src.outcome(slot, cls, S.mat_classes != 0);
 }
 
 // One tile of extend: thread i traces the ray at position tile*256 + i.
-template <class Src, bool SPILL, int CAP, class E, bool CAPPED = false>
+template <class Src, bool SPILL, int CAP, class E>
 PT_DEV void ExtendTile(const dscene& S, const Src& src, uint32_t n, uint32_t* spill, uint32_t spill_stride, E* smem,
-                       uint32_t tile, bool timed, const float4* nc = nullptr, uint32_t ncn = 0,
-                       const dcont* Q = nullptr)
+                       uint32_t tile, bool timed, const float4* nc = nullptr, uint32_t ncn = 0)
 {
     uint64_t t0 = timed ? __builtin_amdgcn_s_memtime() : 0;
     uint32_t slot = tile * 256 + threadIdx.x;
@@ -1220,7 +1168,7 @@ PT_DEV void ExtendTile(const dscene& S, const Src& src, uint32_t n, uint32_t* sp
     st.stride = spill_stride;
     st.nc = nc;
     st.ncn = ncn;
-    ExtendRay<SPILL, CAP, E, Src, CAPPED>(S, src, st, slot, Q);
+    ExtendRay<SPILL, CAP, E>(S, src, st, slot);
     if constexpr (kRendererSource<Src>) {
         if (timed && (threadIdx.x & 63u) == 0)
             src.L.tilecost[tile * 4 + (threadIdx.x >> 6)] = (uint32_t)(__builtin_amdgcn_s_memtime() - t0);
@@ -1238,9 +1186,9 @@ PT_DEV uint32_t NodeCacheFill(const dscene& S, float4* nc)
     return nodes;
 }
 
-template <class Src, bool SPILL, int MINW, int CAP, class E = uint32_t, bool NC = false, bool CAPPED = false>
+template <class Src, bool SPILL, int MINW, int CAP, class E = uint32_t, bool NC = false>
 __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, uint32_t n, uint32_t* spill,
-                                                                  uint32_t spill_stride, dcont Q)
+                                                                  uint32_t spill_stride)
 {
     __shared__ E smem[CAP * 256];
     __shared__ float4 ncache[NC ? 4 * PT_NODE_CACHE_PAIRS : 1];
@@ -1259,62 +1207,7 @@ __global__ __launch_bounds__(256, MINW) void extend_kernel(dscene S, Src src, ui
             timed = true;
         }
     }
-    ExtendTile<Src, SPILL, CAP, E, CAPPED>(S, src, n, spill, spill_stride, smem, tile, timed, ncache, ncn, &Q);
-}
-
-// The continuation of a capped extend: the queued lanes' traversals resumed
-// from their saved state, 256 queue entries per block (a grid-stride loop
-// over the queue: any survivor count, any grid), each ray finished, its hit
-// stored at its own position and its outcome bit set in its wave's word
-// (an atomic OR: the word's other bits were stored by the capped launch).
-// Block 0 zeroes the next round's counter first, also in a guarded round
-// past the target, so a round's counter is zero when its capped extend starts.
-template <int MINW, int CAP, class E, bool NC>
-__global__ __launch_bounds__(256, MINW) void extend_cont_kernel(dscene S, ray_source_slots src, dcont Q)
-{
-    __shared__ E smem[CAP * 256];
-    __shared__ float4 ncache[NC ? 4 * PT_NODE_CACHE_PAIRS : 1];
-    if (blockIdx.x == 0 && threadIdx.x == 0) *Q.clear = 0u;
-    if (src.L.stop && *src.L.stop) return;
-    const uint32_t count = *Q.count;
-    if (blockIdx.x * 256u >= count) return;   // the whole block: before the fill's barrier
-    const uint32_t ncn = NC ? NodeCacheFill(S, ncache) : 0u;
-    tstack<false, CAP, E> st;
-    st.lds = &smem[threadIdx.x];
-    st.spill = nullptr;
-    st.stride = 0;
-    st.nc = ncache;
-    st.ncn = ncn;
-    const E* stk = static_cast<const E*>(Q.stack);
-    for (uint32_t q = blockIdx.x * 256u + threadIdx.x; q < count; q += gridDim.x * 256u) {
-        const uint32_t pos = Q.pos[q];
-        const float4 ot = Q.ot[q], vs = Q.vs[q], cp = Q.cp[q];
-        const uint4 nd = Q.nd[q];
-        const uint2 hh = Q.hh[q];
-        lane_state Ln;
-        SetLevelRay(S, Ln, v3(ot.x, ot.y, ot.z), v3(vs.x, vs.y, vs.z));
-        Ln.Time = ot.w;
-        Ln.Shape = __float_as_uint(vs.w);
-        Ln.C = v3(cp.x, cp.y, cp.z);
-        Ln.Prim = __float_as_uint(cp.w);
-        Ln.na = nd.x;
-        Ln.nb = nd.y;
-        Ln.blas = nd.z;
-        Ln.dT = nd.w & 0xFFFFu;
-        Ln.dB = nd.w >> 16;
-        Ln.HA = hh.x;
-        Ln.HB = hh.y;
-        const uint32_t depth = Ln.dT + Ln.dB;
-        for (uint32_t i = 0; i < depth; i++) st.put(i, stk[(size_t)i * Q.cap + q]);
-        no_stats ns;
-        while (!LaneStep<false, CAP, ray_source_slots, no_stats, true, E>(S, Ln, st, src, pos, ns)) {}
-        src.store(pos, Ln, S.vidx21 != 0);
-        const uint32_t cls = OutcomeClass(S, Ln);
-        if (S.mat_classes || cls == PT_OUTCOME_CLASSES - 1) {
-            uint64_t* m = src.L.outcome + (size_t)(pos >> 8) * (4 * PT_OUTCOME_CLASSES) + ((pos >> 6) & 3u);
-            atomicOr((unsigned long long*)&m[4 * cls], 1ull << (pos & 63u));
-        }
-    }
+    ExtendTile<Src, SPILL, CAP, E>(S, src, n, spill, spill_stride, smem, tile, timed, ncache, ncn);
 }
 
 // Longest-first dispatch order for the next extend: tiles by their slowest
@@ -2082,16 +1975,16 @@ static void LaunchExtendE(const ptd::dscene& S, const Src& src, uint32_t n, uint
     if constexpr (sizeof(E) == 2) {
         if (!spill && S.node_cache) {
             hipLaunchKernelGGL((ptd::extend_kernel<Src, false, PT_EXTEND_MINW, PT_EXTEND_CAP, E, true>), dim3(blocks),
-                               dim3(256), 0, st, S, src, n, spill, n, ptd::dcont{});
+                               dim3(256), 0, st, S, src, n, spill, n);
             return;
         }
     }
     if (spill)
         hipLaunchKernelGGL((ptd::extend_kernel<Src, true, PT_EXTEND_MINW, PT_EXTEND_CAP, E>), dim3(blocks), dim3(256),
-                           0, st, S, src, n, spill, n, ptd::dcont{});
+                           0, st, S, src, n, spill, n);
     else
         hipLaunchKernelGGL((ptd::extend_kernel<Src, false, PT_EXTEND_MINW, PT_EXTEND_CAP, E>), dim3(blocks),
-                           dim3(256), 0, st, S, src, n, spill, n, ptd::dcont{});
+                           dim3(256), 0, st, S, src, n, spill, n);
 }
 
 // n: rays (the spill stride and the bound of the ray index); blocks: the
@@ -2103,39 +1996,6 @@ static hipError_t LaunchExtend(const ptd::dscene& S, const Src& src, uint32_t n,
     if (n == 0 || blocks == 0) return hipSuccess;
     if (S.stack16) LaunchExtendE<Src, uint16_t>(S, src, n, blocks, spill, st);
     else LaunchExtendE<Src, uint32_t>(S, src, n, blocks, spill, st);
-    return hipGetLastError();
-}
-
-template <class E>
-static void LaunchExtendCapped(const ptd::dscene& S, const ptd::ray_source_slots& src, const ptd::dcont& Q,
-                               uint32_t blocks, uint32_t cont_blocks, hipStream_t st)
-{
-    const uint32_t n = src.L.n;
-    if constexpr (sizeof(E) == 2) {
-        if (S.node_cache) {
-            hipLaunchKernelGGL(
-                (ptd::extend_kernel<ptd::ray_source_slots, false, PT_EXTEND_MINW, PT_EXTEND_CAP, E, true, true>),
-                dim3(blocks), dim3(256), 0, st, S, src, n, nullptr, n, Q);
-            hipLaunchKernelGGL((ptd::extend_cont_kernel<PT_EXTEND_MINW, PT_EXTEND_CAP, E, true>), dim3(cont_blocks),
-                               dim3(256), 0, st, S, src, Q);
-            return;
-        }
-    }
-    {
-        hipLaunchKernelGGL((ptd::extend_kernel<ptd::ray_source_slots, false, PT_EXTEND_MINW, PT_EXTEND_CAP, E, false, true>),
-                           dim3(blocks), dim3(256), 0, st, S, src, n, nullptr, n, Q);
-        hipLaunchKernelGGL((ptd::extend_cont_kernel<PT_EXTEND_MINW, PT_EXTEND_CAP, E, false>), dim3(cont_blocks),
-                           dim3(256), 0, st, S, src, Q);
-    }
-}
-
-hipError_t pt_launch_extend_capped(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F,
-                                   const ptd::dcont& Q, uint32_t cont_blocks, hipStream_t st)
-{
-    if (L.n == 0 || L.tile_count == 0) return hipSuccess;
-    if (L.spill || Q.steps == 0 || Q.cap < L.tile_count * 256u || cont_blocks == 0) return hipErrorInvalidValue;
-    if (S.stack16) LaunchExtendCapped<uint16_t>(S, ptd::ray_source_slots{L, F}, Q, L.tile_count, cont_blocks, st);
-    else LaunchExtendCapped<uint32_t>(S, ptd::ray_source_slots{L, F}, Q, L.tile_count, cont_blocks, st);
     return hipGetLastError();
 }
 

@@ -54,26 +54,6 @@ struct dframe {
     float4* accx;             // streams x width x height (streams > 1)
 };
 
-// Continuation queue of the step-capped extend (pt_launch_extend_capped;
-// DESIGN §4 "Compaction across launches").  A capped extend stops every wave
-// after `steps` wave steps; each lane still traversing saves its traversal
-// state here, packed (one atomic per wave), and the continuation launch
-// traces the queue densely.  SoA records, survivor q at index q; stack entry
-// i of survivor q at stack[i * cap + q] (the scene's stack entry width).
-struct dcont {
-    uint32_t* count;    // this round's survivors (the capped extend adds, the continuation reads)
-    uint32_t* clear;    // the next round's counter (the other parity): zeroed by the continuation
-    uint32_t* pos;      // the survivor's ray position
-    float4* ot;         // current-level ray origin, Hit.Time
-    float4* vs;         // current-level ray velocity, Hit.ShapeIndex (bits)
-    float4* cp;         // Hit.PrimitiveCoordinates, Hit.PrimitiveIndex (bits)
-    uint4* nd;          // na, nb, blas, dT | dB << 16
-    uint2* hh;          // HA, HB
-    void* stack;        // [CAP][cap] stack entries
-    uint32_t cap;       // survivors the queue holds (the launch's positions)
-    uint32_t steps;     // wave steps of the capped launch
-};
-
 struct dparams {
     uint32_t camera_index;
     uint32_t render_flags;
@@ -91,12 +71,6 @@ hipError_t pt_launch_raygen(const ptd::dscene& S, const ptd::dslots& L, const pt
                             hipStream_t st);
 hipError_t pt_launch_extend(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* spill,
                             hipStream_t st);
-// Step-capped extend then its continuation over the queue (same stream): the
-// hits, and the ShadeOrder words, of pt_launch_extend, bit for bit.  Needs a
-// renderer without a spilled stack (L.spill null).  cont_blocks: the
-// continuation's grid (it strides over the queue).
-hipError_t pt_launch_extend_capped(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F,
-                                   const ptd::dcont& Q, uint32_t cont_blocks, hipStream_t st);
 hipError_t pt_launch_extend_stats(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, uint32_t* spill,
                                   unsigned long long* out, uint32_t* steps, hipStream_t st);
 // Material-type mask of a scene (shade kernel specialisation).

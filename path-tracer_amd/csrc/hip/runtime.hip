@@ -198,22 +198,6 @@ struct pt_basic_renderer {
     dbuf<float4> accx;                  // streams > 1: each stream's accumulator (streams x width x height)
     uint64_t rays = 0;                  // rays traced since the last Reset
     dbuf<uint32_t> spill;
-    // Step-capped extend (ptSetBasicRendererExtendCap): the continuation
-    // queue, one region per tile group (group g: its dispatch segment's
-    // positions, offset start * 256) or the whole frame (single-stream
-    // rounds), and a counter pair (parities) per region.
-    uint32_t extend_cap = 0;            // 0 automatic, 1 off, S >= 2: S wave steps
-    dbuf<uint32_t> cont_count, cont_pos;
-    dbuf<float4> cont_ot, cont_vs, cont_cp;
-    dbuf<uint4> cont_nd;
-    dbuf<uint2> cont_hh;
-    dbuf<uint8_t> cont_stack;
-    uint32_t cont_parity[PT_MAX_SPLIT + 1] = {};
-    void release_cont()
-    {
-        cont_count.release(); cont_pos.release(); cont_ot.release(); cont_vs.release(); cont_cp.release();
-        cont_nd.release(); cont_hh.release(); cont_stack.release();
-    }
 };
 
 struct pt_comm {
@@ -1116,7 +1100,6 @@ void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
     if (d) { (void)hipSetDevice(d->id); (void)DeviceWait(d); }
     r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->prob1.release(); r->grey_count.release();
     r->cq_counts.release(); r->cq_list.release();
-    r->release_cont();
     r->lam.release();
     r->uv.release(); r->act.release(); r->pos.release(); r->slotof.release(); r->outcome.release();
     r->tilecost.release(); r->order.release();
@@ -1222,78 +1205,6 @@ static bool ShadeCompact(const pt_basic_renderer* r)
            r->scene->d.g.SkyboxSamplingProbability > 0.0f || r->params.PathTerminationProbability > 0.0f;
 }
 
-// Step-capped extend with compaction across launches (kernels.hip
-// extend_kernel<..., CAPPED> + extend_cont_kernel; DESIGN §4 "Compaction
-// across launches"): the wave steps a capped launch runs before its
-// still-traversing lanes are queued, or 0 when the renderer's extends run
-// uncapped.  Automatic: CONT_AUTO_STEPS on scenes whose stack needs no spill
-// rows (the queue holds the LDS stack only).
-constexpr uint32_t CONT_AUTO_STEPS = 32;
-
-static uint32_t ExtendCap(const pt_basic_renderer* r)
-{
-    // (The spill rows are allocated at the first round: the scene's stack
-    // depth decides, as EnsureSpill does.)
-    if (r->scene->stack_needed > pt_extend_stack_cap() || r->slots.spill || r->extend_cap == 1) return 0;
-    return r->extend_cap >= 2 ? r->extend_cap : CONT_AUTO_STEPS;
-}
-
-// The queue: SoA records for every position of the frame (a tile group's
-// region is its own positions' share), stack columns of the scene's entry
-// width, 2 x (PT_MAX_SPLIT + 1) counters, zeroed once.  About 76 B + 20
-// stack entries per slot; allocated on first use.
-static int ContBuffers(pt_basic_renderer* r)
-{
-    const size_t n = r->slots.n;
-    const size_t ew = r->scene->d.stack16 ? 2 : 4;
-    if (r->cont_pos.count >= n && r->cont_stack.count >= n * pt_extend_stack_cap() * ew && r->cont_count.ptr) return 0;
-    r->release_cont();
-    if (r->cont_count.alloc(2 * (PT_MAX_SPLIT + 1)) != hipSuccess || r->cont_pos.alloc(n) != hipSuccess ||
-        r->cont_ot.alloc(n) != hipSuccess || r->cont_vs.alloc(n) != hipSuccess || r->cont_cp.alloc(n) != hipSuccess ||
-        r->cont_nd.alloc(n) != hipSuccess || r->cont_hh.alloc(n) != hipSuccess ||
-        r->cont_stack.alloc(n * pt_extend_stack_cap() * ew) != hipSuccess ||
-        hipMemset(r->cont_count.ptr, 0, 2 * (PT_MAX_SPLIT + 1) * sizeof(uint32_t)) != hipSuccess) {
-        r->release_cont();
-        SetError("continuation queue allocation failed");
-        return -1;
-    }
-    for (uint32_t& p : r->cont_parity) p = 0;
-    return 0;
-}
-
-// Extend of one round over the slots L (a tile group's or every tile) on
-// stream st: capped with its continuation when ExtendCap says so (region:
-// the group index, or PT_MAX_SPLIT for single-stream rounds; first: the
-// region's first position), else the one-launch extend.
-static int LaunchRoundExtend(pt_basic_renderer* r, const ptd::dslots& L, const ptd::dframe& F, uint32_t region,
-                             uint32_t first, hipStream_t st)
-{
-    const uint32_t steps = ExtendCap(r);
-    if (steps == 0) {
-        PT_HIP(pt_launch_extend(r->scene->d, L, F, L.spill, st));
-        return 0;
-    }
-    if (int e = ContBuffers(r)) return e;
-    const size_t ew = r->scene->d.stack16 ? 2 : 4;
-    ptd::dcont Q{};
-    const uint32_t p = r->cont_parity[region];
-    r->cont_parity[region] = p ^ 1u;
-    Q.count = r->cont_count.ptr + 2 * region + p;
-    Q.clear = r->cont_count.ptr + 2 * region + (p ^ 1u);
-    Q.pos = r->cont_pos.ptr + first;
-    Q.ot = r->cont_ot.ptr + first;
-    Q.vs = r->cont_vs.ptr + first;
-    Q.cp = r->cont_cp.ptr + first;
-    Q.nd = r->cont_nd.ptr + first;
-    Q.hh = r->cont_hh.ptr + first;
-    Q.stack = r->cont_stack.ptr + (size_t)first * pt_extend_stack_cap() * ew;
-    Q.cap = L.tile_count * 256u;
-    Q.steps = steps;
-    const uint32_t blocks = std::min<uint32_t>(L.tile_count, std::max<uint32_t>(r->dev->cu_count, 1u) * 4u);
-    PT_HIP(pt_launch_extend_capped(r->scene->d, L, F, Q, blocks, st));
-    return 0;
-}
-
 static bool RoundFused(const pt_basic_renderer* r, const ptd::dslots& g)
 {
     const int mode = r->fused;
@@ -1387,7 +1298,7 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
             if (int e = EndTimed(d, ep)) return e;
         } else {
             if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled)) return e;
-            if (int e = LaunchRoundExtend(r, L, F, PT_MAX_SPLIT, 0, d->stream)) return e;
+            PT_HIP(pt_launch_extend(r->scene->d, L, F, L.spill, d->stream));
             if (int e = EndTimed(d, ep)) return e;
             if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled)) return e;
             if (ClassListRounds(r)) {
@@ -1485,10 +1396,8 @@ static int RunRoundsSplit(pt_device* d, pt_basic_renderer* r, uint64_t k, uint32
     const bool compact = ShadeCompact(r);
     ptd::dslots G[PT_MAX_SPLIT];
     hipStream_t S[PT_MAX_SPLIT];
-    uint32_t first[PT_MAX_SPLIT];   // the group's continuation-queue region
     for (uint32_t g = 0; g < K; g++) {
         G[g] = r->slots;
-        first[g] = pt_tile_group_start(r->slots.tile_count, K, g) * 256u;
         G[g].order = r->slots.order + pt_tile_group_start(r->slots.tile_count, K, g);
         G[g].tile_count = pt_tile_group_count(r->slots.tile_count, K, g);
         S[g] = g ? d->group_stream[g - 1] : d->stream;
@@ -1513,7 +1422,7 @@ static int RunRoundsSplit(pt_device* d, pt_basic_renderer* r, uint64_t k, uint32
                 event_pair ep{};
                 if (g == 0)
                     if (int e = BeginTimed(d, PT_KERNEL_EXTEND, ep, sampled)) return e;
-                if (int e = LaunchRoundExtend(r, G[g], F, g, first[g], S[g])) return e;
+                PT_HIP(pt_launch_extend(r->scene->d, G[g], F, r->slots.spill, S[g]));
                 if (g == 0) {
                     if (int e = EndTimed(d, ep)) return e;
                     if (int e = BeginTimed(d, PT_KERNEL_SHADE, ep, sampled)) return e;
@@ -1624,20 +1533,6 @@ int ptGetBasicRendererClassLists(const pt_basic_renderer* r, uint32_t* used)
     return 0;
 }
 
-int ptSetBasicRendererExtendCap(pt_basic_renderer* r, uint32_t steps)
-{
-    if (!r) { SetError("ptSetBasicRendererExtendCap: null renderer"); return -1; }
-    r->extend_cap = steps;
-    return 0;
-}
-
-int ptGetBasicRendererExtendCap(const pt_basic_renderer* r, uint32_t* steps)
-{
-    if (!r || !steps) { SetError("ptGetBasicRendererExtendCap: null argument"); return -1; }
-    *steps = ExtendCap(r);
-    return 0;
-}
-
 int ptSetBasicRendererSplit(pt_basic_renderer* r, uint32_t groups)
 {
     if (!r || groups > PT_MAX_SPLIT) {
@@ -1718,7 +1613,7 @@ static int RunGuardedRounds(pt_device* d, pt_basic_renderer* r, uint32_t n, uint
         if (fused) {
             PT_HIP(pt_launch_round(r->scene->d, L, F, P, mats, d->stream));
         } else {
-            if (int e = LaunchRoundExtend(r, L, F, PT_MAX_SPLIT, 0, d->stream)) return e;
+            PT_HIP(pt_launch_extend(r->scene->d, L, F, L.spill, d->stream));
             if (lists) {
                 if (int e = ClassListShade(d, r, L, F, P, d->stream)) return e;
             } else {

@@ -295,18 +295,6 @@ class BasicRenderer:
                "ptGetBasicRendererSplit")
         return {"groups": int(g.value), "timed_tiles": int(t0.value), "tiles": int(t.value)}
 
-    def set_extend_cap(self, steps: int):
-        """Step-capped extend with a compacted continuation launch
-        (ptSetBasicRendererExtendCap): 0 automatic, 1 off, S >= 2 wave steps.
-        Results are identical for every value."""
-        _check(N.hip_lib().ptSetBasicRendererExtendCap(self._h, int(steps)), "ptSetBasicRendererExtendCap")
-
-    def extend_cap(self) -> int:
-        """The wave-step cap the renderer's extends use now (0: uncapped)."""
-        u = C.c_uint32(0)
-        _check(N.hip_lib().ptGetBasicRendererExtendCap(self._h, C.byref(u)), "ptGetBasicRendererExtendCap")
-        return int(u.value)
-
     def set_class_lists(self, mode: int):
         """Class-pure shade inside tile groups (ptSetBasicRendererClassLists):
         0 automatic, 1 off.  Results are identical either way."""

@@ -24,7 +24,6 @@ def main():
     ap.add_argument("--fused", type=int, default=0, help="ptSetBasicRendererFusedRounds mode (0 never, 1 auto)")
     ap.add_argument("--batch", type=int, default=1, help="round batch for the timed rounds (1: one launch pair each)")
     ap.add_argument("--split", type=int, default=0, help="tile groups (ptSetBasicRendererSplit; 0 automatic, 1 off)")
-    ap.add_argument("--extend-cap", type=int, default=0, help="ptSetBasicRendererExtendCap (0 automatic, 1 off, S)")
     a = ap.parse_args()
     if a.lib:
         os.environ["PT_HIP_LIB"] = str((ROOT / a.lib) if not os.path.isabs(a.lib) else a.lib)
@@ -41,8 +40,6 @@ def main():
     r.set_fused_rounds(a.fused)
     r.set_round_batch(a.batch)
     r.set_split(a.split)
-    if hasattr(r, "set_extend_cap"):
-        r.set_extend_cap(a.extend_cap)
     r.RenderFlags = info.render_flags
     r.PathTerminationProbability = info.termination_probability
     r.reset()
