@@ -288,3 +288,33 @@ def test_class_lists_not_for_single_material(pt, dev):
     r.close()
     sb.close()
     ds.close()
+
+
+@pytest.mark.parametrize("config,W,H", [(2, 160, 128), (5, 192, 96)])
+def test_class_list_block_orders(pt, dev, config, W, H):
+    """The class-pure shade's block orders (class by class, interleaved,
+    interleaved in XCD slabs; ptSetBasicRendererClassListOrder) in tile
+    groups and in single-stream rounds: the same bits as the unsplit
+    tile-local rounds."""
+    s = scene_for(pt, config)
+    ds = pt.DeviceScene(dev)
+    ds.update(s)
+    ref = render(pt, dev, ds, W, H, [1, 1], [6, 5])
+    for order in (0, 1, 2):
+        sb = pt.SampleBuffer(dev, W, H)
+        r = pt.BasicRenderer(dev, ds, sb)
+        r.RenderFlags = 3
+        r.set_fused_rounds(0)
+        r.set_class_list_order(order)
+        r.set_split(3)
+        assert r.class_lists()
+        r.reset()
+        r.run(2)          # single-stream rounds through the lists
+        r.run_rounds(6)
+        r.run(1)
+        r.run_rounds(4)
+        dev.synchronize()
+        same((r.read_state(), sb.read(), r.stats()), ref)
+        r.close()
+        sb.close()
+    ds.close()
