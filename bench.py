@@ -311,8 +311,6 @@ def main():
                     help="tile groups on concurrent streams (ptSetBasicRendererSplit): 0 automatic, 1 off, K")
     ap.add_argument("--class-lists", type=int, default=0,
                     help="class-pure shade in tile groups (ptSetBasicRendererClassLists): 0 automatic, 1 off")
-    ap.add_argument("--class-order", type=int, default=-1,
-                    help="class-pure shade block order (ptSetBasicRendererClassListOrder; -1: the library default)")
     ap.add_argument("--streams", type=int, default=0,
                     help="path streams per owned pixel (0: auto -- bands fill ~2^21 slots per launch, samples 1)")
     ap.add_argument("--inject-failure", type=int, default=-1, metavar="RANK",
@@ -378,8 +376,6 @@ def main():
     r.set_split(args.split)
     try:
         r.set_class_lists(args.class_lists)
-        if args.class_order >= 0:
-            r.set_class_list_order(args.class_order)
         class_lists = r.class_lists()
     except AttributeError:   # an older library under PT_HIP_LIB (A/B builds)
         class_lists = None

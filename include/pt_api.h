@@ -265,12 +265,6 @@ int                ptSetBasicRendererRoundBatch(pt_basic_renderer* renderer, uin
  * them now.  Default 0. */
 int                ptSetBasicRendererClassLists(pt_basic_renderer* renderer, uint32_t mode);
 int                ptGetBasicRendererClassLists(const pt_basic_renderer* renderer, uint32_t* used);
-/* Order of the class-pure shade's blocks: 0 = class by class; 1 =
- * interleaved, every class sweeping the tiles at the same pace (path records
- * that one class's waves leave in a cache line are read by the other
- * classes' waves while the line is in L2); 2 = interleaved, each XCD taking
- * one contiguous eighth of that order.  Results are identical. */
-int                ptSetBasicRendererClassListOrder(pt_basic_renderer* renderer, uint32_t order);
 int                ptSetBasicRendererSplit(pt_basic_renderer* renderer, uint32_t groups);
 int                ptGetBasicRendererSplit(const pt_basic_renderer* renderer, uint32_t* groups, uint32_t* timed_tiles,
                                            uint32_t* tiles);

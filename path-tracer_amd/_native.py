@@ -259,7 +259,6 @@ HIP_API = {
     "ptRunBasicRendererRounds": (_i32, [_vp, _vp, _u32]),
     "ptSetBasicRendererRoundBatch": (_i32, [_vp, _u32]),
     "ptSetBasicRendererSplit": (_i32, [_vp, _u32]),
-    "ptSetBasicRendererClassListOrder": (_i32, [_vp, _u32]),
     "ptSetBasicRendererClassLists": (_i32, [_vp, _u32]),
     "ptGetBasicRendererClassLists": (_i32, [_vp, _u32ptr]),
     "ptGetBasicRendererSplit": (_i32, [_vp, _u32ptr, _u32ptr, _u32ptr]),

@@ -1709,47 +1709,9 @@ __global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void shade_kernel(dscen
 // address per C2 round, serialised, 26 us).  Block 0 clears the other
 // parity's counters for the next round.
 constexpr uint32_t CQ_TILES = 16;
-// Interleaved block order (class_order >= 1): the shade blocks of all
-// classes in one sequence ordered by how far through its class's list each
-// block is -- block j of b_k blocks of class k at (2j + 1) / (2 b_k), ties by
-// class -- so every class sweeps the group's tiles at the same time and the
-// path records a wave of one class leaves in a cache line are read by the
-// other classes' waves while the line is still in L2 (class-major order
-// swept each class over the whole group before the next).  The last list
-// block to finish (a ticket) writes table[rank] = class << 24 | j; the rank
-// of (k, j) is j plus, per other class k', the blocks j' with
-// (2 j' + 1) b_k < (2 j + 1) b_k' (<= when k' < k).
-PT_DEV void ClassOrderTable(const uint32_t* counts, uint32_t* table)
-{
-    constexpr uint32_t C = PT_OUTCOME_CLASSES;
-    uint32_t b[C], cum[C + 1];
-    cum[0] = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < C; k++) {
-        b[k] = (atomicAdd(const_cast<uint32_t*>(&counts[k]), 0u) + 255u) / 256u;
-        cum[k + 1] = cum[k] + b[k];
-    }
-    for (uint32_t e = threadIdx.x; e < cum[C]; e += 256) {
-        uint32_t k = 0;
-#pragma unroll
-        for (uint32_t h = 1; h < C; h++) k += e >= cum[h] ? 1u : 0u;
-        const uint32_t j = e - cum[k];
-        uint32_t rank = j;
-#pragma unroll
-        for (uint32_t h = 0; h < C; h++) {
-            if (h == k || b[h] == 0) continue;
-            const uint64_t A = (uint64_t)(2u * j + 1u) * b[h];
-            const uint64_t m = h < k ? A / b[k] : (A - 1u) / b[k];
-            rank += (uint32_t)min<uint64_t>((m + 1u) / 2u, b[h]);
-        }
-        table[rank] = (k << 24) | j;
-    }
-}
-
 __global__ __launch_bounds__(256) void class_list_kernel(dslots L, uint32_t mat_classes, uint32_t* counts,
                                                          uint32_t* next_counts, uint32_t* list, uint32_t capk,
-                                                         uint32_t tiles_all, uint32_t groups, uint32_t group,
-                                                         uint32_t* order_table, uint32_t* ticket)
+                                                         uint32_t tiles_all, uint32_t groups, uint32_t group)
 {
     // L.tile_count tiles of tile group `group` (all tiles: groups = 1).
     if (L.stop && *L.stop) return;   // a guarded round past the frame's target
@@ -1802,17 +1764,6 @@ __global__ __launch_bounds__(256) void class_list_kernel(dslots L, uint32_t mat_
             }
         }
     }
-    if (!order_table) return;
-    // The last block to finish sees every block's counter update.
-    __shared__ uint32_t last;
-    __threadfence();
-    __syncthreads();
-    if (t == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1u;
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    ClassOrderTable(counts, order_table);
-    if (t == 0) atomicExch(ticket, 0u);   // the next round's
 }
 
 template <uint32_t MATS, bool COMPACT>
@@ -1820,9 +1771,7 @@ __global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void shade_classq_kerne
                                                                                          dparams Pm,
                                                                                          const uint32_t* counts,
                                                                                          const uint32_t* list,
-                                                                                         uint32_t capk,
-                                                                                         const uint32_t* order_table,
-                                                                                         uint32_t xcd_slabs)
+                                                                                         uint32_t capk)
 {
     constexpr uint32_t C = PT_OUTCOME_CLASSES;
     if (L.stop && *L.stop) return;   // a guarded round past the frame's target
@@ -1837,34 +1786,12 @@ __global__ __launch_bounds__(256, ShadeMinWaves<MATS>()) void shade_classq_kerne
         tot[k] = x;
     }
     uint32_t c = C, i0 = 0, n = 0, start = 0;
-    if (order_table) {
-        // Interleaved order (ClassOrderTable); xcd_slabs: the blocks the
-        // dispatcher sends to XCD x (blockIdx % 8 == x) take the x-th eighth
-        // of that order, so one XCD's L2 holds a slab of the group's tiles.
-        uint32_t total = 0;
 #pragma unroll
-        for (uint32_t k = 0; k < C; k++) total += (tot[k] + 255u) / 256u;
-        uint32_t B = blockIdx.x;
-        if (xcd_slabs) {
-            const uint32_t per = (total + 7u) / 8u;
-            if ((blockIdx.x >> 3) >= per) return;   // whole block: past its XCD's slab
-            B = (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
-        }
-        if (B >= total) return;   // whole block: past every list
-        const uint32_t e = order_table[B];
-        c = e >> 24;
-        i0 = (e & 0xFFFFFFu) * 256u;
-#pragma unroll
-        for (uint32_t k = 0; k < C; k++)
-            if (k == c) n = tot[k];
-    } else {
-#pragma unroll
-        for (uint32_t k = 0; k < C; k++) {
-            const uint32_t nk = tot[k];
-            const uint32_t bk = (nk + 255u) / 256u;
-            if (c == C && blockIdx.x < start + bk) { c = k; i0 = (blockIdx.x - start) * 256u; n = nk; }
-            start += bk;
-        }
+    for (uint32_t k = 0; k < C; k++) {
+        const uint32_t nk = tot[k];
+        const uint32_t bk = (nk + 255u) / 256u;
+        if (c == C && blockIdx.x < start + bk) { c = k; i0 = (blockIdx.x - start) * 256u; n = nk; }
+        start += bk;
     }
     if (c == C) return;   // whole block: past every list
     const uint32_t i = i0 + threadIdx.x;
@@ -2332,23 +2259,18 @@ hipError_t pt_launch_shade(const ptd::dscene& S, const ptd::dslots& L, const ptd
 
 template <bool COMPACT>
 static void LaunchShadeQ(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F, const ptd::dparams& P,
-                         uint32_t scene_mats, const uint32_t* counts, const uint32_t* list, const uint32_t* table,
-                         uint32_t order, hipStream_t st)
+                         uint32_t scene_mats, const uint32_t* counts, const uint32_t* list, hipStream_t st)
 {
     // The shade instantiations of LaunchShade for scenes with more than one
     // material type (pt_class_lists_supported); blocks past the lists return.
-    // (Every class's blocks: at most tiles + classes; rounded up to whole
-    // XCD rows for the slab mapping.)
-    const uint32_t blocks = (L.tile_count + ptd::PT_OUTCOME_CLASSES + 7u) / 8u * 8u + 8u;
+    const uint32_t blocks = L.tile_count + ptd::PT_OUTCOME_CLASSES;
     const uint32_t capk = pt_classq_sub_capacity(L.tile_count);
-    const uint32_t* tb = order ? table : nullptr;
-    const uint32_t slabs = order == 2 ? 1u : 0u;
     if (pt_shade_mats(scene_mats) == (PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_SCENE))
         hipLaunchKernelGGL((ptd::shade_classq_kernel<PT_MATS_DIFFUSE | PT_MATS_METAL | PT_MATS_SCENE, COMPACT>),
-                           dim3(blocks), dim3(256), 0, st, S, L, F, P, counts, list, capk, tb, slabs);
+                           dim3(blocks), dim3(256), 0, st, S, L, F, P, counts, list, capk);
     else
         hipLaunchKernelGGL((ptd::shade_classq_kernel<PT_MATS_ALL | PT_MATS_SCENE, COMPACT>), dim3(blocks), dim3(256), 0,
-                           st, S, L, F, P, counts, list, capk, tb, slabs);
+                           st, S, L, F, P, counts, list, capk);
 }
 
 bool pt_class_lists_supported(uint32_t scene_mats)
@@ -2360,17 +2282,15 @@ bool pt_class_lists_supported(uint32_t scene_mats)
 hipError_t pt_launch_shade_classq(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F,
                                   const ptd::dparams& P, uint32_t scene_mats, bool compact, uint32_t* counts,
                                   uint32_t* next_counts, uint32_t* list, hipStream_t st, uint32_t tiles_all,
-                                  uint32_t groups, uint32_t group, uint32_t* order_table, uint32_t* ticket,
-                                  uint32_t order)
+                                  uint32_t groups, uint32_t group)
 {
     if (L.n == 0 || L.tile_count == 0) return hipSuccess;
     if (!pt_class_lists_supported(scene_mats)) return hipErrorNotSupported;
-    if (order && (!order_table || !ticket)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(ptd::class_list_kernel, dim3((L.tile_count + ptd::CQ_TILES - 1) / ptd::CQ_TILES), dim3(256), 0,
                        st, L, S.mat_classes, counts, next_counts, list, pt_classq_sub_capacity(L.tile_count),
-                       tiles_all ? tiles_all : L.tile_count, groups, group, order ? order_table : nullptr, ticket);
-    if (compact) LaunchShadeQ<true>(S, L, F, P, scene_mats, counts, list, order_table, order, st);
-    else LaunchShadeQ<false>(S, L, F, P, scene_mats, counts, list, order_table, order, st);
+                       tiles_all ? tiles_all : L.tile_count, groups, group);
+    if (compact) LaunchShadeQ<true>(S, L, F, P, scene_mats, counts, list, st);
+    else LaunchShadeQ<false>(S, L, F, P, scene_mats, counts, list, st);
     return hipGetLastError();
 }
 

@@ -127,11 +127,7 @@ bool pt_class_lists_supported(uint32_t scene_mats);
 hipError_t pt_launch_shade_classq(const ptd::dscene& S, const ptd::dslots& L, const ptd::dframe& F,
                                   const ptd::dparams& P, uint32_t scene_mats, bool compact, uint32_t* counts,
                                   uint32_t* next_counts, uint32_t* list, hipStream_t st, uint32_t tiles_all = 0,
-                                  uint32_t groups = 1, uint32_t group = 0, uint32_t* order_table = nullptr,
-                                  uint32_t* ticket = nullptr, uint32_t order = 0);
-// order: 0 class-major blocks; 1 interleaved (kernels.hip ClassOrderTable:
-// order_table holds tiles + classes + 16 words, ticket one word, zero between
-// rounds); 2 interleaved, each XCD taking one slab of the order.
+                                  uint32_t groups = 1, uint32_t group = 0);
 hipError_t pt_launch_vertex_decode(const uint2* v, uint32_t n, float4* attr, float* vv, hipStream_t st);
 // Tile groups (ptSetBasicRendererSplit): group g of K owns tiles g, g + K, ...
 // (pt_tile_group_count of them) and the dispatch-order segment starting at

@@ -174,8 +174,6 @@ struct pt_basic_renderer {
     bool grey_blocked = false;          // some live path cannot take it (until the next Reset / state write)
     dbuf<uint32_t> grey_count;          // pt_launch_grey_check's result word
     dbuf<uint32_t> cq_counts, cq_list;  // class-pure shade lists (ClassLists)
-    dbuf<uint32_t> cq_table, cq_ticket; // their shade blocks' interleaved order, per region (ClassListBuffers)
-    uint32_t class_order = 0;           // ptSetBasicRendererClassListOrder: 0 class-major, 1 interleaved, 2 + XCD slabs
     uint32_t cq_parity = 0;
     uint32_t class_lists = 0;           // ptSetBasicRendererClassLists: 0 automatic, 1 off
     dbuf<float> lam;                    // lambda0 per slot (Sample is 0 between rounds)
@@ -1101,7 +1099,7 @@ void ptDestroyBasicRenderer(pt_device* d, pt_basic_renderer* r)
     if (!r) return;
     if (d) { (void)hipSetDevice(d->id); (void)DeviceWait(d); }
     r->ray.release(); r->hit.release(); r->thr.release(); r->prob.release(); r->prob1.release(); r->grey_count.release();
-    r->cq_counts.release(); r->cq_list.release(); r->cq_table.release(); r->cq_ticket.release();
+    r->cq_counts.release(); r->cq_list.release();
     r->lam.release();
     r->uv.release(); r->act.release(); r->pos.release(); r->slotof.release(); r->outcome.release();
     r->tilecost.release(); r->order.release();
@@ -1230,19 +1228,13 @@ static size_t ClassListStride(uint32_t tiles, uint32_t K)
 // ClassListStride) or for a single-stream round over every tile, whichever
 // is larger (about 20 B per slot), grown when K grows.  A growth waits for
 // the device stream: the old lists may still be read by queued launches.
-// The interleaved block order's table of one region (kernels.hpp).
-static uint32_t ClassTableStride(uint32_t tiles) { return tiles + ptd::PT_OUTCOME_CLASSES + 16u; }
-
 static int ClassListBuffers(pt_device* d, pt_basic_renderer* r, uint32_t K)
 {
     const size_t nc = (size_t)ptd::PT_OUTCOME_CLASSES * CQ_SUB;
     const uint32_t T = r->slots.tile_count;
     if (!r->cq_counts.ptr) {
         if (r->cq_counts.alloc((PT_MAX_SPLIT + 1) * 2 * nc) != hipSuccess ||
-            hipMemset(r->cq_counts.ptr, 0, (PT_MAX_SPLIT + 1) * 2 * nc * sizeof(uint32_t)) != hipSuccess ||
-            r->cq_table.alloc((PT_MAX_SPLIT + 1) * (size_t)ClassTableStride(T)) != hipSuccess ||
-            r->cq_ticket.alloc(PT_MAX_SPLIT + 1) != hipSuccess ||
-            hipMemset(r->cq_ticket.ptr, 0, (PT_MAX_SPLIT + 1) * sizeof(uint32_t)) != hipSuccess) {
+            hipMemset(r->cq_counts.ptr, 0, (PT_MAX_SPLIT + 1) * 2 * nc * sizeof(uint32_t)) != hipSuccess) {
             SetError("class list allocation failed");
             return -1;
         }
@@ -1277,8 +1269,7 @@ static int ClassListShade(pt_device* d, pt_basic_renderer* r, const ptd::dslots&
     uint32_t* cq_next = cnt + nc * (r->cq_parity ^ 1u);
     r->cq_parity ^= 1u;
     PT_HIP(pt_launch_shade_classq(r->scene->d, L, F, P, ShadeMats(r), ShadeCompact(r), cq, cq_next, r->cq_list.ptr,
-                                  st, 0, 1, 0, r->cq_table.ptr + (size_t)PT_MAX_SPLIT * ClassTableStride(L.tile_count),
-                                  r->cq_ticket.ptr + PT_MAX_SPLIT, r->class_order));
+                                  st));
     return 0;
 }
 
@@ -1444,9 +1435,7 @@ static int RunRoundsSplit(pt_device* d, pt_basic_renderer* r, uint64_t k, uint32
                     PT_HIP(pt_launch_shade_classq(r->scene->d, G[g], F, P, mats, compact, cnt + nc * (i & 1u),
                                                   cnt + nc * ((i & 1u) ^ 1u),
                                                   r->cq_list.ptr + g * ClassListStride(r->slots.tile_count, K), S[g],
-                                                  r->slots.tile_count, K, g,
-                                                  r->cq_table.ptr + (size_t)g * ClassTableStride(r->slots.tile_count),
-                                                  r->cq_ticket.ptr + g, r->class_order));
+                                                  r->slots.tile_count, K, g));
                 } else {
                     PT_HIP(pt_launch_shade(r->scene->d, G[g], F, P, mats, compact, S[g]));
                 }
@@ -1534,13 +1523,6 @@ int ptSetBasicRendererClassLists(pt_basic_renderer* r, uint32_t mode)
 {
     if (!r || mode > 1) { SetError("ptSetBasicRendererClassLists: bad argument (0 automatic, 1 off)"); return -1; }
     r->class_lists = mode;
-    return 0;
-}
-
-int ptSetBasicRendererClassListOrder(pt_basic_renderer* r, uint32_t order)
-{
-    if (!r || order > 2) { SetError("ptSetBasicRendererClassListOrder: bad argument (0, 1, 2)"); return -1; }
-    r->class_order = order;
     return 0;
 }
 

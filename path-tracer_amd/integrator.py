@@ -300,11 +300,6 @@ class BasicRenderer:
         0 automatic, 1 off.  Results are identical either way."""
         _check(N.hip_lib().ptSetBasicRendererClassLists(self._h, int(mode)), "ptSetBasicRendererClassLists")
 
-    def set_class_list_order(self, order: int):
-        """Block order of the class-pure shade (ptSetBasicRendererClassListOrder):
-        0 class by class, 1 interleaved, 2 interleaved in XCD slabs."""
-        _check(N.hip_lib().ptSetBasicRendererClassListOrder(self._h, int(order)), "ptSetBasicRendererClassListOrder")
-
     def class_lists(self) -> bool:
         """Whether consecutive rounds shade through per-class lists now."""
         u = C.c_uint32(0)

@@ -83,7 +83,6 @@ def test_null_arguments_rejected(pt):
     assert L.ptWriteBasicRendererState(None, None, None) != 0
     assert L.ptGetBasicRendererShadeInfo(None, None) != 0
     assert L.ptReadBasicRendererStreamAccumulator(None, None, 0, None) != 0
-    assert L.ptSetBasicRendererClassListOrder(None, 1) != 0
     assert L.ptSetBasicRendererSplit(None, 2) != 0
     assert L.ptGetBasicRendererSplit(None, None, None, None) != 0
     assert L.ptSetBasicRendererClassLists(None, 0) != 0

@@ -291,30 +291,28 @@ def test_class_lists_not_for_single_material(pt, dev):
 
 
 @pytest.mark.parametrize("config,W,H", [(2, 160, 128), (5, 192, 96)])
-def test_class_list_block_orders(pt, dev, config, W, H):
-    """The class-pure shade's block orders (class by class, interleaved,
-    interleaved in XCD slabs; ptSetBasicRendererClassListOrder) in tile
-    groups and in single-stream rounds: the same bits as the unsplit
-    tile-local rounds."""
+def test_class_lists_uneven_groups_and_single_rounds(pt, dev, config, W, H):
+    """Class lists with tile groups that do not divide the tiles evenly (80
+    and 72 tiles in three groups: the list buffers grow from the
+    single-stream size to three group regions) and single-stream list rounds
+    between split batches: the same bits as the unsplit tile-local rounds."""
     s = scene_for(pt, config)
     ds = pt.DeviceScene(dev)
     ds.update(s)
     ref = render(pt, dev, ds, W, H, [1, 1], [6, 5])
-    for order in (0, 1, 2):
-        sb = pt.SampleBuffer(dev, W, H)
-        r = pt.BasicRenderer(dev, ds, sb)
-        r.RenderFlags = 3
-        r.set_fused_rounds(0)
-        r.set_class_list_order(order)
-        r.set_split(3)
-        assert r.class_lists()
-        r.reset()
-        r.run(2)          # single-stream rounds through the lists
-        r.run_rounds(6)
-        r.run(1)
-        r.run_rounds(4)
-        dev.synchronize()
-        same((r.read_state(), sb.read(), r.stats()), ref)
-        r.close()
-        sb.close()
+    sb = pt.SampleBuffer(dev, W, H)
+    r = pt.BasicRenderer(dev, ds, sb)
+    r.RenderFlags = 3
+    r.set_fused_rounds(0)
+    r.set_split(3)
+    assert r.class_lists()
+    r.reset()
+    r.run(2)          # single-stream rounds through the lists
+    r.run_rounds(6)
+    r.run(1)
+    r.run_rounds(4)
+    dev.synchronize()
+    same((r.read_state(), sb.read(), r.stats()), ref)
+    r.close()
+    sb.close()
     ds.close()

@@ -1,6 +1,8 @@
-"""Debug: class-list rounds at a frame size whose tiles do not split evenly
-into three groups, against the oracle after every call (which call first
-differs, and where)."""
+"""Debug aid: a renderer's schedule against the oracle after every call --
+which call first differs, how many pixels and state fields.
+
+usage: python tools/exp_lists_debug.py CONFIG W H r2,b6,r1,b4 [SPLIT]
+       (r = run(k), b = run_rounds(k); SPLIT: tile groups, default 3)"""
 import sys
 from pathlib import Path
 
@@ -17,8 +19,7 @@ def main():
     pt = ge._load_package()
     config, W, H = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
     sched = sys.argv[4].split(",")   # e.g. r2,b6,r1,b4  (r = run(k), b = run_rounds(k))
-    order = int(sys.argv[5]) if len(sys.argv) > 5 else 0
-    split = int(sys.argv[6]) if len(sys.argv) > 6 else 3
+    split = int(sys.argv[5]) if len(sys.argv) > 5 else 3
     s = pt.Scene.config(config)
     dev = pt.Device(0)
     ds = pt.DeviceScene(dev)
@@ -27,7 +28,6 @@ def main():
     r = pt.BasicRenderer(dev, ds, sb)
     r.RenderFlags = 3
     r.set_fused_rounds(0)
-    r.set_class_list_order(order)
     r.set_split(split)
     print("class lists", r.class_lists(), "split", r.split(), flush=True)
     o = oracle_lib.OracleRenderer(s.packs(), W, H)
