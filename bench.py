@@ -174,17 +174,31 @@ def settled_oracle(scene, width, height, threads, flags, settle_rounds=CPU_SETTL
     return o
 
 
-def time_oracle_rounds(o, threads, min_rounds=32, max_seconds=30.0):
+def pin_cores(threads):
+    """(cores, placement): `threads` distinct physical cores of one package
+    for the CPU leg (pick_cores), as a sorted list, or (None, reason) when
+    that is every affinity CPU or the topology is unreadable."""
+    if threads >= len(os.sched_getaffinity(0)):
+        return None, "every affinity CPU, unpinned"
+    pinned, placement = pick_cores(threads)
+    return (sorted(pinned) if pinned else None), placement
+
+
+def time_oracle_rounds(o, threads, min_rounds=32, max_seconds=30.0, cores=None, placement=None):
     """Time consecutive single rounds of a settled oracle at `threads`
-    threads, pinned to that many distinct physical cores of one package
-    (pick_cores) unless that is every affinity CPU: at least min_rounds, more
-    while under max_seconds / 2, never past max_seconds.  The one timing
-    code path of bench.py's CPU leg and tools/cpu_scaling.py's table."""
+    threads, pinned to `cores` (distinct physical cores of one package:
+    pin_cores; the first `threads` of them) or unpinned when None: at least
+    min_rounds, more while under max_seconds / 2, never past max_seconds.
+    The one timing code path of bench.py's CPU leg and tools/cpu_scaling.py's
+    table."""
     home = os.sched_getaffinity(0)
     o.set_threads(threads)
     # The oracle's worker threads are created per round and inherit this
     # thread's mask.
-    pinned, placement = pick_cores(threads) if threads < len(home) else (None, "every affinity CPU, unpinned")
+    pinned = set(cores[:threads]) if cores else None
+    if placement is None:
+        placement = (f"{threads} threads pinned to {threads} distinct physical cores" if pinned
+                     else "every affinity CPU, unpinned")
     try:
         if pinned:
             os.sched_setaffinity(0, pinned)
@@ -223,11 +237,22 @@ def cpu_baseline(pt, scene, width, height, config, settle_rounds=CPU_SETTLE_ROUN
     about 15-30 s of CPU work."""
     threads, allowed, omp = cpu_threads()
     host_cpus = os.cpu_count() or 1
-    o = settled_oracle(scene, width, height, threads, 3, settle_rounds)
+    # Pinned from the oracle's creation on, so its worker threads first-touch
+    # the path state on the package they then run on (settling it unpinned
+    # left pages on the other package of the NUMA host: 8.98 against 11.76
+    # Mrays/s on one box, profiles/r06_final).
+    cores, placement = pin_cores(threads)
+    home = os.sched_getaffinity(0)
     try:
-        row = time_oracle_rounds(o, threads, min_rounds, max_seconds)
+        if cores:
+            os.sched_setaffinity(0, set(cores))
+        o = settled_oracle(scene, width, height, threads, 3, settle_rounds)
+        try:
+            row = time_oracle_rounds(o, threads, min_rounds, max_seconds, cores, placement)
+        finally:
+            o.close()
     finally:
-        o.close()
+        os.sched_setaffinity(0, home)
     share = "the job's CPU share (OMP_NUM_THREADS)" if omp > 0 and omp < allowed else "every affinity CPU"
     return {
         "value": row["mrays_per_s"],

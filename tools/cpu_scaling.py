@@ -1,10 +1,10 @@
 """Thread scaling of the CPU baseline (the oracle: scalar C++ restatement of
 the integrator, std::thread over pixels) on the C3 frame, 1..T threads.
 
-One code path with bench.py's CPU leg: bench.settled_oracle
-(Reset, Run(2), 34 settle rounds) and bench.time_oracle_rounds (threads
-pinned to distinct physical cores of one package, at least 32 rounds, more
-while under 15 s).  The table's first row IS the bench leg: a fresh oracle at
+One code path with bench.py's CPU leg: bench.pin_cores (the
+threads' distinct physical cores of one package, pinned from the oracle's
+creation on), bench.settled_oracle (Reset, Run(2), 34 settle rounds) and
+bench.time_oracle_rounds (at least 32 rounds, more while under 15 s).  The table's first row IS the bench leg: a fresh oracle at
 the job's thread count, settled and timed exactly as bench.py times it.  The
 other thread counts then time the rounds that follow on the same render
 (oracle_set_threads), largest first.
@@ -47,7 +47,15 @@ def main():
             t //= 2
             counts.append(t)
     counts = sorted(set(counts), reverse=True)
+    # The bench leg's placement: pinned from creation on (first touch on the
+    # package the threads run on); smaller counts take the first cores of
+    # that set, so every row runs on the package that holds the state.
+    cores, placement = bench.pin_cores(counts[0])
+    home = os.sched_getaffinity(0)
+    if cores:
+        os.sched_setaffinity(0, set(cores))
     o = bench.settled_oracle(scene, info.width, info.height, counts[0], 3)
+    os.sched_setaffinity(0, home)
     rows = []
     for i, t in enumerate(counts):
         # The first row: bench.py's CPU leg exactly (fresh settled render,
@@ -56,7 +64,7 @@ def main():
         mx = a.max_seconds if i == 0 else min(a.max_seconds, 20.0)
         est = rows[0]["median_round_s"] * counts[0] / t if rows else 0.0   # this count's round, predicted
         mn = a.rounds if i == 0 else max(4, min(a.rounds, int(mx / max(est, 1e-3))))
-        row = bench.time_oracle_rounds(o, t, mn, mx)
+        row = bench.time_oracle_rounds(o, t, mn, mx, cores, placement if i == 0 else None)
         row["bench_leg"] = i == 0 and t == lead
         rows.append(row)
         print(json.dumps(row), flush=True)
