@@ -1285,6 +1285,30 @@ int ptRunBasicRenderer(pt_device* d, pt_basic_renderer* r, uint32_t rounds)
     ptd::dframe F = Frame(r);
     const ptd::dslots& L = r->slots;
     const bool fused = RoundFused(r, L);
+    // Run(R >= 2) where round batches apply (RunRounds' rule): the R rounds
+    // with the one seed as batches of the rounds kernel (seed_step 0), one
+    // launch instead of R -- the application's Run(2) after a restart.
+    const uint32_t B = r->round_batch ? r->round_batch : (fused && r->fused == 1 ? AUTO_BATCH : 1u);
+    if (fused && rounds >= 2 && B >= 2 && pt_rounds_available(L)) {
+        for (uint32_t left = rounds; left > 0;) {
+            const uint32_t n = std::min(left, B);
+            ptd::dparams Pb = P;
+            Pb.rounds = n;
+            Pb.seed_step = 0;
+            const uint64_t t = d->run_tick % d->profile_period;
+            const bool sampled = d->profiling && (t == 0 || t + n > d->profile_period);
+            d->run_tick += n;
+            event_pair ep{};
+            if (int e = BeginTimed(d, PT_KERNEL_ROUNDS, ep, sampled, n)) return e;
+            PT_HIP(pt_launch_rounds(r->scene->d, L, F, Pb, ShadeMats(r), d->stream));
+            if (int e = EndTimed(d, ep)) return e;
+            for (uint32_t g = 0; g < r->order_groups; g++)
+                PT_HIP(pt_launch_tile_order(L, d->stream, r->order_groups, g));
+            r->rays += r->valid_slots * n;
+            left -= n;
+        }
+        return 0;
+    }
     for (uint32_t i = 0; i < rounds; i++) {
         // Kernel timing samples every profile_period-th round.
         const bool sampled = d->profiling && (d->run_tick++ % d->profile_period) == 0;

@@ -248,14 +248,20 @@ def test_profiling_counts_kernels(pt, dev):
     # one extend + one shade per round
     assert n_ext == n_sh == 3 and ms_ext > 0 and ms_sh > 0
     assert dev.kernel_rounds(1) == 3 and dev.kernel_rounds(2) == 3
-    # a 64x64 frame fits the GPU at once: the automatic mode fuses its rounds
-    # into one launch each (kernel 5)
+    # a 64x64 frame fits the GPU at once: the automatic mode fuses a round
+    # into one launch (kernel 5), and the rounds of one Run(R) into one
+    # round batch (kernel 6, seed step 0)
     dev.reset_kernel_stats()
     r.set_fused_rounds(1)
-    r.run(2)
+    r.run(1)
     n_rd, ms_rd = dev.kernel_stats(5)
     assert dev.kernel_stats(1)[0] == 0 and dev.kernel_stats(2)[0] == 0
-    assert n_rd == 2 and dev.kernel_rounds(5) == 2 and ms_rd > 0
+    assert n_rd == 1 and dev.kernel_rounds(5) == 1 and ms_rd > 0
+    dev.reset_kernel_stats()
+    r.run(2)
+    n_rb, ms_rb = dev.kernel_stats(6)
+    assert dev.kernel_stats(5)[0] == 0 and dev.kernel_stats(1)[0] == 0
+    assert n_rb == 1 and dev.kernel_rounds(6) == 2 and ms_rb > 0
     # consecutive Run(1) rounds of such a frame run as 16-round batches
     # (kernel 6, PT_KERNEL_ROUNDS): a timed batch counts its rounds, and the
     # profiling period counts rounds (period 8: every batch holds a sampled
