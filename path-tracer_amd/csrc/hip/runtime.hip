@@ -1679,9 +1679,10 @@ constexpr double GUARD_PREDICTED = 8.0;   // rounds left, by the last batch's ra
 // target is already reached (RunGuardedRounds), so a rate that changes can
 // cost a read-back but never a round.  The guarded end starts with the
 // rounds that cannot overshoot, batched, and guards only the rest.  The
-// rate decides only how the rounds are issued, never how many run.  Measured on the C3 1024-spp frame
-// (tools/exp_frame_end.py, profiles/r06_frame_end): 16 batches, +2 ms
-// (0.19 %) against the same 2 760 rounds in one call with no read-back.
+// rate decides only how the rounds are issued, never how many run.
+// Measured on the C3 1024-spp frame (tools/exp_frame_end.py,
+// profiles/r06_frame_end): 16 batches, +1.7 ms (0.16 %) against the same
+// 2 760 rounds in one call with no read-back.
 int ptRenderFrame(pt_device* d, pt_basic_renderer* r, uint64_t target_samples, uint32_t max_rounds,
                   uint32_t* rounds_out, uint64_t* samples_out)
 {
