@@ -282,6 +282,9 @@ int                ptGetStats(pt_device* device, pt_basic_renderer* renderer, ui
  * application loop of application.cpp:100-115 with an spp target): Reset,
  * Run(2), then Run(1) rounds until the paths completed since the Reset reach
  * target_samples (e.g. spp * pixels owned) or max_rounds (>= 2) rounds ran.
+ * The frame always ends at the first round whose total reaches the target,
+ * as the loop issued one round at a time would (the rounds are batched only
+ * where they cannot overshoot, the last few guarded on the device).
  * Blocks until done.  rounds_out / samples_out (either may be NULL): rounds
  * run and paths completed. */
 int                ptRenderFrame(pt_device* device, pt_basic_renderer* renderer, uint64_t target_samples,
