@@ -62,7 +62,7 @@ def framed(pt, dev, ds, W, H, target, max_rounds, fused):
 
 
 @pytest.mark.parametrize("config,W,H,fused", [(1, 256, 256, 1), (3, 320, 180, 0), (2, 128, 128, 0)])
-@pytest.mark.parametrize("spp,max_rounds", [(16, 1 << 30), (16, 9), (16, 5), (3, 1 << 30)])
+@pytest.mark.parametrize("spp,max_rounds", [(16, 1 << 30), (16, 9), (16, 5), (16, 20), (16, 22), (3, 1 << 30)])
 def test_frame_equals_round_by_round_loop(pt, dev, config, W, H, fused, spp, max_rounds):
     s = scene_for(pt, config)
     ds = pt.DeviceScene(dev)

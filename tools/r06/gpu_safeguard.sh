@@ -6,6 +6,6 @@ O=$R/gpurun_out/${1:-r06_safeguard}
 mkdir -p "$O"
 export TMPDIR=/tmp
 cd "$R"
-timeout -k 10 700 python -u -m pytest tests/test_gpu_frame.py tests/test_gpu_bench_path.py -v -m gpu -x --timeout 400 --timeout-method thread -k "frame" > "$O/tests.log" 2>&1
+timeout -k 10 700 python -u -m pytest tests/test_gpu_frame.py -v -m gpu -x --timeout 400 --timeout-method thread > "$O/tests.log" 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 "$O/tests.log"; [ $rc -eq 0 ] || exit $rc
 bash tools/r06/gpu_ab_lib.sh ${1:-r06_safeguard} "1 3 2" base head
