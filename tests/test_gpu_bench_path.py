@@ -26,7 +26,7 @@ from test_gpu_parity import compare_state, scene_for
 
 pytestmark = pytest.mark.gpu
 
-FULL = {2: (1024, 1024), 3: (1920, 1080), 5: (2048, 1024)}
+FULL = {2: (1024, 1024), 3: (1920, 1080), 4: (3840, 2160), 5: (2048, 1024)}
 
 
 @pytest.fixture(scope="module")
@@ -65,12 +65,12 @@ def oracle_for(pt, config, W, H):
     return o
 
 
-@pytest.mark.parametrize("config", [3, 2, 5])
+@pytest.mark.parametrize("config", [3, 2, 5, 4])
 def test_split_rounds_full_size_vs_oracle(pt, dev, config):
     """Reset, Run(2), then run_rounds(7) and run_rounds(5): two split batches
     (fork and join on the group streams, a tile-order re-sort inside them,
     class-list parities across the batch boundary) against 2 + 12 oracle
-    rounds."""
+    rounds.  C4 is the 4K room on one GPU (8.3 M slots, 32 400 tiles)."""
     W, H = FULL[config]
     s = scene_for(pt, config)
     ds = pt.DeviceScene(dev)
